@@ -1,0 +1,273 @@
+#!/usr/bin/env python3
+"""bench.py — Msamples/s (rays x bounces per second) of the HIP path-tracing megakernel.
+
+Workload (BASELINE.json configs[1]): Cornell-34 scene, 1920x1080, 64 spp, 8 bounces.
+One step = the whole workload once: 64 frames of every pixel (running-average accumulation,
+frames 0..63) through libhippt's C ABI.  With N GPUs (torchrun, one process per GPU) the
+image is split into N contiguous row bands, one per rank (strong scaling: the image is fixed);
+no collective touches the data path — ranks only meet at the barriers and the max-over-ranks
+of the timed interval (gloo, CPU).
+
+value = segments traced by all ranks in the K timed steps / max-over-ranks wall time, in
+millions per second; the segment count is the exact count the kernel accumulates (one per
+closest-hit query), so nothing is estimated.
+
+Also reported on rank 0:
+  roofline      the mesh kernel's algorithmic bytes per launch / its mean launch time (HIP
+                events on the library's stream, timed region), against the 8 TB/s HBM peak;
+                bytes per launch from a counted (untimed) pass: 64 B per BVH node visit,
+                48 B per triangle test, 32 B per shaded hit, 12 B per sample written
+                (DESIGN.md §Roofline).  traffic = PMC-measured HBM bytes per launch from
+                profiles/ when a matching summary exists, else null.
+  cpu_baseline  the reference CPU path tracer (RayTracer.h + Qt-free RenderWorker, built as
+                oracle/_ref/ref_harness) timed on this box's host cores over a bounded row
+                sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "qt-raytracer_amd"))
+
+METRIC = "Msamples/s (rays×bounces/s) at 1920×1080, 8 bounces; 1/2/4/8-GPU scaling"
+HBM_PEAK_GBS = 8000.0
+BYTES_NODE, BYTES_TRI, BYTES_SHADE, BYTES_SAMPLE = 64, 48, 32, 12
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def parse():
+    p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--scene", default="cornell34", choices=["cornell34", "blob70k"])
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--spp", type=int, default=64)
+    p.add_argument("--depth", type=int, default=8)
+    p.add_argument("--wave-threshold", type=int, default=None)
+    p.add_argument("--chunk", type=int, default=None)
+    p.add_argument("--scratch-mb", type=int, default=None)
+    p.add_argument("--cpu-baseline", default="auto", choices=["auto", "reference", "port", "off"])
+    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU sample duration")
+    p.add_argument("--cpu-threads", type=int, default=None)
+    p.add_argument("--pmc", default=None, help="PMC summary JSON for roofline.traffic")
+    return p.parse_args()
+
+
+def cpu_threads(args) -> int:
+    if args.cpu_threads:
+        return args.cpu_threads
+    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return max(1, min(n if n > 0 else (os.cpu_count() or 1), 16))
+
+
+def cpu_baseline(args, scene) -> dict | None:
+    """Reference CPU tracer on a bounded sample of rows of the same workload."""
+    if args.cpu_baseline == "off":
+        return None
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle  # checker / baseline only
+    from hippt import scenes as sc_mod
+    threads = cpu_threads(args)
+    kind = args.cpu_baseline
+    if kind == "auto":
+        kind = "reference" if os.path.exists(pyoracle.REF_HARNESS) else "port"
+    if kind == "reference":
+        with tempfile.TemporaryDirectory() as tmp:
+            path = os.path.join(tmp, "scene.bin")
+            sc_mod.write_scene_file(scene, path)
+
+            def run(rows):
+                out = subprocess.run([pyoracle.REF_HARNESS, "bench", path, str(args.width), str(args.height),
+                                      str(rows), str(args.spp), str(args.depth), str(threads)],
+                                     capture_output=True, text=True, check=True, timeout=600).stdout
+                return json.loads(out.strip().splitlines()[-1])
+
+            probe = run(max(1, min(24, args.height)))
+            rows = int(probe["rows"] * args.cpu_seconds / max(probe["seconds"], 1e-3))
+            rows = max(1, min(args.height, rows))
+            r = run(rows)
+        return {"value": round(r["msamples_per_s"], 4), "unit": "Msamples/s", "cores": threads,
+                "kind": "reference",
+                "sample": f"rows 0..{rows - 1} of {args.width}x{args.height}, {args.spp} spp, depth {args.depth}, "
+                          f"{scene.name}; RayTracer.h ray_color + RenderWorker tile pool (tile {r['tile']}), "
+                          f"{r['segments']} segments in {r['seconds']:.2f} s",
+                "mpixel_samples_per_s": round(r["mpixel_samples_per_s"], 4)}
+    ms = pyoracle.MeshScene(scene, args.width, args.height, accel=1)
+    t0 = time.perf_counter()
+    _, _, segs, ps = ms.frames(0, args.spp, args.depth, y0=0, y1=2, nthreads=threads)
+    rate = segs / max(time.perf_counter() - t0, 1e-6)
+    rows = max(1, min(args.height, int(args.cpu_seconds * rate / max(segs / 2, 1))))
+    t0 = time.perf_counter()
+    _, _, segs, ps = ms.frames(0, args.spp, args.depth, y0=0, y1=rows, nthreads=threads)
+    dt = time.perf_counter() - t0
+    return {"value": round(segs / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"rows 0..{rows - 1}, {args.spp} spp, depth {args.depth}, {scene.name}; FP32 oracle port"}
+
+
+def load_pmc(args, workload: str):
+    path = args.pmc or os.path.join(REPO, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None
+    if d.get("workload") != workload:
+        return None
+    return d.get("hbm_bytes_per_launch")
+
+
+def main():
+    args = parse()
+    import torch  # noqa: F401  (torch.distributed for the rank barrier / max-over-ranks)
+    import torch.distributed as dist
+    import hippt
+    from hippt import distributed as hd
+    from hippt import scenes
+
+    rank, local_rank, world = hd.env_rank()
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    if world != args.gpus:
+        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
+    lib = hippt.load_library()
+    ndev = lib.hipptDeviceCount()
+    if ndev < 1:
+        raise SystemExit("no HIP device visible")
+    device = local_rank % ndev
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    def device_sync(pt):
+        if not pt.synchronize():
+            raise SystemExit(pt.lastError())
+        if torch.cuda.is_available():
+            torch.cuda.set_device(device)
+            torch.cuda.synchronize()
+
+    scene = scenes.get_scene(args.scene)
+    y0, y1 = hd.row_band(rank, world, args.height)
+    pt = hippt.PathTracer()
+    pt.setDevices([device])
+    pt.setRowRange(y0, y1)
+    if args.wave_threshold is not None:
+        pt.setOption(hippt.OPT_WAVE_THRESHOLD, args.wave_threshold)
+    if args.chunk is not None:
+        pt.setOption(hippt.OPT_CHUNK, args.chunk)
+    if args.scratch_mb is not None:
+        pt.setOption(hippt.OPT_SCRATCH_MB, args.scratch_mb)
+    pt.uploadMesh(scene)
+    if not pt.initialize(args.width, args.height):
+        raise SystemExit(pt.lastError())
+
+    def step():
+        # frames 0..spp-1: frame 0 overwrites the accumulation (acc*0 + L), so every step is
+        # the identical full workload
+        if not pt._lib.hipptRenderFramesAsync(0, args.spp, args.depth, None):
+            raise SystemExit(hippt.load_library().hipptLastError().decode())
+
+    # counted pass (untimed): traversal counters for the roofline's algorithmic bytes
+    pt.setOption(hippt.OPT_COUNT_TRAVERSAL, 1)
+    pt.resetStats()
+    step()
+    device_sync(pt)
+    counted = pt.stats()
+    pt.setOption(hippt.OPT_COUNT_TRAVERSAL, 0)
+
+    for _ in range(args.warmup):
+        step()
+    device_sync(pt)
+    pt.resetStats()
+
+    barrier()
+    device_sync(pt)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    device_sync(pt)
+    barrier()
+    elapsed = time.perf_counter() - t0
+
+    st = pt.stats()
+    elapsed_max = hd.max_over_ranks(elapsed, dist)
+    segments = hd.sum_over_ranks(st["segments"], dist)
+    samples = hd.sum_over_ranks(st["pixelSamples"], dist)
+    value = segments / elapsed_max / 1e6
+
+    # output image of the last step: gathered bands (untimed), checksum on rank 0
+    px, _ = pt.readback(y0, y1)
+    full = hd.gather_bands(px, args.height, dist)
+
+    # roofline of the dominant (mesh) kernel, from this rank's counted pass and live events
+    launches = max(1, st["traceLaunches"] // max(1, args.steps))
+    alg_bytes_step = (BYTES_NODE * counted["nodeVisits"] + BYTES_TRI * counted["triTests"]
+                      + BYTES_SHADE * (counted["segments"] - counted["pixelSamples"])
+                      + BYTES_SAMPLE * counted["pixelSamples"])
+    alg_bytes_launch = alg_bytes_step / launches
+    mean_launch_ms = st["traceMs"] / max(1, st["traceLaunches"])
+    achieved = alg_bytes_launch / (mean_launch_ms * 1e-3) / 1e9 if mean_launch_ms > 0 else 0.0
+    workload = f"{args.scene} {args.width}x{args.height} {args.spp}spp depth{args.depth}"
+    traffic = load_pmc(args, workload)
+
+    if rank == 0:
+        cpu = cpu_baseline(args, scene) if world == 1 else None
+        import zlib
+        line = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "Msamples/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed_max * 1e3 / args.steps, 4),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic",
+            "config": {
+                "workload": workload + " (BASELINE configs[1])" if args.scene == "cornell34" and args.width == 1920
+                and args.height == 1080 and args.spp == 64 and args.depth == 8 else workload,
+                "scene": args.scene, "triangles": scene.num_tris, "width": args.width, "height": args.height,
+                "spp": args.spp, "max_depth": args.depth, "parallelism": f"row-bands x{world}",
+                "segments_per_step": segments // max(1, args.steps),
+                "pixel_samples_per_step": samples // max(1, args.steps),
+                "mpixel_samples_per_s": round(samples / elapsed_max / 1e6, 3),
+                "trace_ms_per_step": round(st["traceMs"] / args.steps, 4),
+                "combine_ms_per_step": round(st["combineMs"] / args.steps, 4),
+                "bvh_nodes": st["bvhNodes"], "bvh_depth": st["bvhDepth"],
+                "wave_threshold": pt._lib.hipptGetOption(hippt.OPT_WAVE_THRESHOLD),
+                "chunk": pt._lib.hipptGetOption(hippt.OPT_CHUNK),
+                "image_crc32": zlib.crc32(full.tobytes()) & 0xFFFFFFFF,
+            },
+            "roofline": {
+                "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "kernel": "mesh_kernel", "mean_launch_ms": round(mean_launch_ms, 4),
+                "launches_per_step": launches,
+                "alg_bytes_per_launch": int(alg_bytes_launch),
+                "node_visits_per_step": counted["nodeVisits"], "tri_tests_per_step": counted["triTests"],
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

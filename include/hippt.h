@@ -1,0 +1,150 @@
+/*
+ * hippt.h — C ABI of libhippt.so, the MI355X-native (gfx950) path-tracing backend.
+ *
+ * Drop-in boundary.  The first three entry points are EXACTLY the reference's
+ * CUDA backend ABI, so CudaPathTracer.cpp links unchanged with
+ * ENABLE_CUDA_BACKEND defined:
+ *
+ *   cudaPathTracerInit      replaces CudaPathTracerKernel.cu:188-237  (declared CudaPathTracer.cpp:5)
+ *   cudaPathTracerRender    replaces CudaPathTracerKernel.cu:239-276  (declared CudaPathTracer.cpp:6)
+ *   cudaPathTracerShutdown  replaces CudaPathTracerKernel.cu:278-288  (declared CudaPathTracer.cpp:7)
+ *
+ * Semantics kept from the reference: Init frees previous buffers and may be called
+ * repeatedly (RayTracerFboItem.cpp:520-521 re-inits on frame 0); Render renders ONE
+ * sample per pixel for the caller-supplied frameIndex (running average,
+ * CudaPathTracerKernel.cu:157-169), blocks until the frame is on the host and returns
+ * a library-owned W*H ARGB array (row 0 = v = 0) valid until the next Init/Shutdown;
+ * errors are `false` + a library-owned message (null out-pointers allowed); Shutdown is
+ * idempotent.  Unlike the reference, every entry point is serialised by an internal
+ * mutex (the reference is called from two Qt threads without a lock).
+ *
+ * The default scene is the reference kernel's built-in 4-sphere scene
+ * (CudaPathTracerKernel.cu:113-116).  The hippt* extensions add triangle-mesh scenes
+ * (host SAH BVH build + upload), batched multi-sample rendering, multi-GPU row bands,
+ * and counters.  The GL-backend shape (GpuPathTracer.h:9-38: renderFrame(spp, depth),
+ * resetAccumulation) maps onto hipptRenderFrames / hipptResetAccumulation.
+ *
+ * No torch types, no HIP types: plain pointers and sizes.
+ */
+#ifndef HIPPT_H
+#define HIPPT_H
+
+#include <stdbool.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- reference ABI (CudaPathTracer.cpp:4-8) ---------------------------------- */
+bool cudaPathTracerInit(int width, int height, const char **errorMessage);
+bool cudaPathTracerRender(int frameIndex, int maxDepth, const unsigned int **hostPixels,
+                          const char **errorMessage);
+void cudaPathTracerShutdown(void);
+
+/* Same functions under backend-neutral names. */
+bool hipPathTracerInit(int width, int height, const char **errorMessage);
+bool hipPathTracerRender(int frameIndex, int maxDepth, const unsigned int **hostPixels,
+                         const char **errorMessage);
+void hipPathTracerShutdown(void);
+
+/* ---- scene description ---------------------------------------------------------- */
+/* Camera as the kernels consume it: RayTracer.h Camera (:545-561) computed in FP64 and
+ * stored FP32.  Layout is part of the ABI (80 bytes). */
+typedef struct hipptCamera {
+    float origin[3], llc[3], horizontal[3], vertical[3], u[3], v[3];
+    float lens_radius;
+    float reserved;
+} hipptCamera;
+
+/* Builds a camera exactly like RayTracer.h Camera::Camera (:545-561). */
+void hipptBuildCamera(const double lookfrom[3], const double lookat[3], const double vup[3], double vfovDeg,
+                      double aspect, double aperture, double focusDist, hipptCamera *out);
+
+enum { HIPPT_SCENE_SPHERE4 = 0, HIPPT_SCENE_MESH = 1 };
+
+/* Selects the reference built-in 4-sphere scene (the default). */
+bool hipptUseBuiltinScene(int sceneId, const char **errorMessage);
+
+/* Triangle mesh: verts = numTris*9 floats (v0,v1,v2), triMaterial = numTris ints in
+ * [0,numMaterials), albedo = numMaterials*3 floats (Lambertian, RayTracer.h:473-488).
+ * Builds a binned-SAH BVH on the host and uploads it to every device on the next render.
+ * The camera is given by RayTracer.h Camera parameters; the aspect ratio is width/height
+ * of the current Init (as RayTracerFboItem.cpp:49-56 does). */
+bool hipptUploadMesh(const float *verts, const int *triMaterial, int numTris, const float *albedo,
+                     int numMaterials, const double lookfrom[3], const double lookat[3], const double vup[3],
+                     double vfovDeg, double aperture, double focusDist, const char **errorMessage);
+
+/* Optional: replace the camera by a prebuilt one (used as-is, whatever the aspect). */
+bool hipptSetCamera(const hipptCamera *camera, const char **errorMessage);
+
+/* ---- devices and row bands ------------------------------------------------------- */
+int hipptDeviceCount(void);
+/* Render on these devices (one context per device, contiguous row bands); takes effect
+ * at the next Init.  Default: the current HIP device only. */
+bool hipptSetDevices(const int *deviceIds, int numDevices, const char **errorMessage);
+/* Restrict this process to rows [y0, y1) of the image (one-process-per-GPU launch);
+ * y1 <= 0 means "to the last row".  Takes effect at the next Init. */
+bool hipptSetRowRange(int y0, int y1, const char **errorMessage);
+
+/* ---- rendering ------------------------------------------------------------------- */
+/* Renders `count` samples per pixel as frames firstFrame..firstFrame+count-1; the
+ * accumulation buffer ends exactly as after `count` single-frame Render calls.  Blocks
+ * until the image is on the host (hostPixels may be null to skip the copy). */
+bool hipptRenderFrames(int firstFrame, int count, int maxDepth, const unsigned int **hostPixels,
+                       const char **errorMessage);
+/* Enqueues the same work without waiting and without a device-to-host copy. */
+bool hipptRenderFramesAsync(int firstFrame, int count, int maxDepth, const char **errorMessage);
+bool hipptSynchronize(const char **errorMessage);
+/* Copies the current image (ARGB, W*H) and/or accumulation buffer (RGBA float, W*H*4)
+ * of the process's row range into caller memory; rows outside the range are untouched. */
+bool hipptReadback(unsigned int *pixels, float *accum, const char **errorMessage);
+/* Zeroes the accumulation buffer (GpuPathTracer::resetAccumulation, GpuPathTracer.cpp:85-95). */
+bool hipptResetAccumulation(const char **errorMessage);
+
+/* ---- counters and options ---------------------------------------------------------- */
+typedef struct hipptStats {
+    unsigned long long segments;      /* closest-hit queries traced (rays x bounces) */
+    unsigned long long pixelSamples;  /* pixel samples rendered */
+    unsigned long long nodeVisits;    /* BVH interior nodes visited (HIPPT_OPT_COUNT_TRAVERSAL) */
+    unsigned long long triTests;      /* ray-triangle tests (HIPPT_OPT_COUNT_TRAVERSAL) */
+    double traceMs;                   /* summed device time of the path-trace kernel launches */
+    double combineMs;                 /* summed device time of the accumulate kernel launches */
+    int traceLaunches;
+    int combineLaunches;
+    int bvhNodes;                     /* scene info */
+    int bvhDepth;
+    int numTris;
+    int numDevices;
+} hipptStats;
+
+bool hipptGetStats(hipptStats *out);
+void hipptResetStats(void);
+
+enum {
+    HIPPT_OPT_COUNT_TRAVERSAL = 1,  /* 1: count node visits / triangle tests (slower) */
+    HIPPT_OPT_WAVE_THRESHOLD = 2,   /* lanes still traversing below which a wave goes to shade */
+    HIPPT_OPT_SCRATCH_MB = 3,       /* cap of the per-batch sample scratch per device */
+    HIPPT_OPT_CHUNK = 4,            /* work items a wave takes from the global queue at once */
+    HIPPT_OPT_BLOCKS_PER_CU = 5     /* persistent-grid residency (0 = occupancy query) */
+};
+bool hipptSetOption(int key, long long value);
+long long hipptGetOption(int key);
+
+const char *hipptLastError(void);
+
+/* ---- host BVH builder (exposed for C++ hosts and tests) ------------------------------- */
+/* Node = 16 x 32-bit words: child-0 box (lo xyz, hi xyz), child-1 box, child0, child1,
+ * 2 reserved.  child >= 0: interior node index; child < 0: leaf, ~child = first<<4 | count. */
+typedef struct hipptBvh hipptBvh;
+hipptBvh *hipptBvhBuild(const float *verts, int numTris, float extentHint, const char **errorMessage);
+int hipptBvhNodeCount(const hipptBvh *bvh);
+int hipptBvhDepth(const hipptBvh *bvh);
+/* nodes: NodeCount*16 words; triOrder: numTris ints (leaf order -> original triangle index). */
+void hipptBvhCopy(const hipptBvh *bvh, uint32_t *nodes, int *triOrder);
+void hipptBvhFree(hipptBvh *bvh);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,35 @@
+// bvh_builder.h — host-side binned-SAH BVH builder for the HIP megakernel.
+//
+// Replaces the reference's BVHNode constructor (RayTracer.h:393-429: random split axis,
+// full sort, median split, pointer tree of shared_ptr<Hitable>) with a flat,
+// GPU-traversable layout.  Only the closest-hit RESULT must match the reference; the
+// tree shape is free.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace hippt {
+
+// Stack entries the kernel keeps per lane in LDS; the builder guarantees that no
+// traversal needs more (interior levels <= kStackDepth).
+constexpr int kStackDepth = 32;
+constexpr int kMaxLeafTris = 4;
+constexpr int kNodeWords = 16;  // 64 B: two child boxes + two child codes
+
+struct Bvh {
+    std::vector<uint32_t> nodes;  // kNodeWords per interior node; node 0 is the root
+    std::vector<int> order;       // leaf order -> original triangle index
+    int levels = 0;               // interior levels on the deepest path (= max stack use)
+    int leaves = 0;
+};
+
+// verts: numTris * 9 floats.  extentHint: largest |coordinate| any ray origin can have
+// (camera position); boxes are padded by max(|coord|, extentHint) * 2^-16 so the
+// kernel's FMA slab test is conservative.
+bool build_bvh(const float *verts, int numTris, float extentHint, Bvh &out, std::string &err);
+
+inline int32_t leaf_code(int first, int count) { return ~((first << 4) | count); }
+
+}  // namespace hippt

@@ -1,0 +1,700 @@
+// hippt_api.cpp — C ABI of libhippt.so (include/hippt.h).
+//
+// Owns all device state, like the reference's single global CudaState
+// (CudaPathTracerKernel.cu:12-21), but:
+//   * one context per device, each rendering a contiguous row band of the image
+//     (multi-GPU; no collective — bands are gathered on the host);
+//   * every entry point is serialised by a mutex (the reference is called from the GUI
+//     thread and the QSG render thread without a lock, RayTracerFboItem.cpp:261,521,529);
+//   * triangle-mesh scenes with a host-built SAH BVH in addition to the reference's
+//     built-in 4-sphere scene.
+#include "../../include/hippt.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "bvh_builder.h"
+#include "hippt_device.h"
+
+struct hipptBvh {
+    hippt::Bvh bvh;
+};
+
+namespace {
+
+using hippt::CameraF;
+
+struct EventPair {
+    hipEvent_t a = nullptr, b = nullptr;
+};
+
+struct Ctx {
+    int device = 0;
+    int y0 = 0, y1 = 0;  // image rows of this band
+    hipStream_t stream = nullptr;
+    float4 *accum = nullptr;
+    uint32_t *out = nullptr;
+    float *scratch = nullptr;
+    size_t scratchBytes = 0;
+    unsigned *queue = nullptr;
+    unsigned long long *stats = nullptr;
+    int sceneVersion = -1;
+    float4 *nodes = nullptr, *tris = nullptr, *shade = nullptr, *albedo = nullptr;
+    int cus = 0, meshBlocksPerCu[2] = {0, 0};
+    std::vector<EventPair> pool;                         // reusable events
+    std::vector<std::pair<int, EventPair>> pending;      // (0 trace / 1 combine, events)
+    size_t poolUsed = 0;
+};
+
+struct SceneHost {
+    int kind = HIPPT_SCENE_SPHERE4;
+    int version = 0;
+    std::vector<float4> nodes, tris, shade, albedo;
+    int numTris = 0, numNodes = 0, levels = 0;
+    double lookfrom[3] = {0, 0, 0}, lookat[3] = {0, 0, -1}, vup[3] = {0, 1, 0};
+    double vfov = 90, aperture = 0, focus = 1;
+    bool rawCamera = false;
+    CameraF cam{};
+};
+
+struct State {
+    std::mutex mu;
+    bool ready = false;
+    int width = 0, height = 0;
+    int rowY0 = 0, rowY1 = 0;
+    std::vector<int> devices;
+    std::vector<Ctx> ctxs;
+    unsigned *host = nullptr;  // pinned W*H ARGB frame (library-owned, as gState.hostOutput)
+    size_t hostCount = 0;
+    SceneHost scene;
+    char error[256] = {0};
+    // options
+    bool countTraversal = false;
+    int waveThreshold = 16;
+    long long scratchMB = 256;
+    unsigned chunk = 256;
+    int blocksPerCu = 0;
+    // host-side timing accumulators
+    double traceMs = 0, combineMs = 0;
+    int traceLaunches = 0, combineLaunches = 0;
+};
+
+State &S() {
+    static State s;
+    return s;
+}
+
+bool fail(const char **errorMessage, const std::string &msg) {
+    State &s = S();
+    std::strncpy(s.error, msg.c_str(), sizeof(s.error) - 1);
+    s.error[sizeof(s.error) - 1] = '\0';
+    if (errorMessage) *errorMessage = s.error;
+    return false;
+}
+
+#define HIP_TRY(expr)                                                                     \
+    do {                                                                                  \
+        hipError_t e_ = (expr);                                                           \
+        if (e_ != hipSuccess) return fail(err, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+// ---- fp32 helpers with the oracle's contract (explicit fma only) ---------------------------
+inline float fdot(const float *a, const float *b) { return std::fmaf(a[0], b[0], std::fmaf(a[1], b[1], a[2] * b[2])); }
+inline void fcross(const float *a, const float *b, float *o) {
+    o[0] = std::fmaf(a[1], b[2], -(a[2] * b[1]));
+    o[1] = std::fmaf(a[2], b[0], -(a[0] * b[2]));
+    o[2] = std::fmaf(a[0], b[1], -(a[1] * b[0]));
+}
+inline float as_float(int v) {
+    float f;
+    std::memcpy(&f, &v, 4);
+    return f;
+}
+
+// RayTracer.h Camera::Camera (:545-561), FP64, stored FP32.
+void build_camera(const double lookfrom[3], const double lookat[3], const double vup[3], double vfov,
+                  double aspect, double aperture, double focus, CameraF &out) {
+    const double pi = 3.1415926535897932385;
+    const double theta = vfov * pi / 180.0;
+    const double h = std::tan(theta / 2);
+    const double vh = 2.0 * h, vw = aspect * vh;
+    auto unit = [](const double a[3], double o[3]) {
+        const double len = std::sqrt(a[0] * a[0] + a[1] * a[1] + a[2] * a[2]);
+        const double inv = 1.0 / len;
+        o[0] = inv * a[0];
+        o[1] = inv * a[1];
+        o[2] = inv * a[2];
+    };
+    auto cross = [](const double a[3], const double b[3], double o[3]) {
+        o[0] = a[1] * b[2] - a[2] * b[1];
+        o[1] = a[2] * b[0] - a[0] * b[2];
+        o[2] = a[0] * b[1] - a[1] * b[0];
+    };
+    double wv[3] = {lookfrom[0] - lookat[0], lookfrom[1] - lookat[1], lookfrom[2] - lookat[2]};
+    double w[3], u[3], v[3], c[3];
+    unit(wv, w);
+    cross(vup, w, c);
+    unit(c, u);
+    cross(w, u, v);
+    for (int i = 0; i < 3; ++i) {
+        const double hor = (focus * vw) * u[i];
+        const double ver = (focus * vh) * v[i];
+        const double llc = ((lookfrom[i] - 0.5 * hor) - 0.5 * ver) - focus * w[i];
+        out.origin[i] = float(lookfrom[i]);
+        out.llc[i] = float(llc);
+        out.horizontal[i] = float(hor);
+        out.vertical[i] = float(ver);
+        out.u[i] = float(u[i]);
+        out.v[i] = float(v[i]);
+    }
+    out.lens_radius = float(aperture / 2);
+    out.reserved = 0.0f;
+}
+
+void free_scene_buffers(Ctx &c) {
+    (void)hipFree(c.nodes);
+    (void)hipFree(c.tris);
+    (void)hipFree(c.shade);
+    (void)hipFree(c.albedo);
+    c.nodes = c.tris = c.shade = c.albedo = nullptr;
+    c.sceneVersion = -1;
+}
+
+void destroy_ctx(Ctx &c) {
+    (void)hipSetDevice(c.device);
+    if (c.stream) (void)hipStreamSynchronize(c.stream);
+    (void)hipFree(c.accum);
+    (void)hipFree(c.out);
+    (void)hipFree(c.scratch);
+    (void)hipFree(c.queue);
+    (void)hipFree(c.stats);
+    free_scene_buffers(c);
+    for (auto &e : c.pool) {
+        (void)hipEventDestroy(e.a);
+        (void)hipEventDestroy(e.b);
+    }
+    if (c.stream) (void)hipStreamDestroy(c.stream);
+    c = Ctx();
+}
+
+void destroy_all() {
+    State &s = S();
+    for (auto &c : s.ctxs) destroy_ctx(c);
+    s.ctxs.clear();
+    if (s.host) (void)hipHostFree(s.host);
+    s.host = nullptr;
+    s.hostCount = 0;
+    s.ready = false;
+}
+
+bool next_events(Ctx &c, EventPair &ev, const char **err) {
+    if (c.poolUsed == c.pool.size()) {
+        EventPair e;
+        HIP_TRY(hipEventCreate(&e.a));
+        HIP_TRY(hipEventCreate(&e.b));
+        c.pool.push_back(e);
+    }
+    ev = c.pool[c.poolUsed++];
+    return true;
+}
+
+bool ensure_scene(Ctx &c, const char **err) {
+    State &s = S();
+    if (s.scene.kind != HIPPT_SCENE_MESH || c.sceneVersion == s.scene.version) return true;
+    free_scene_buffers(c);
+    auto up = [&](float4 *&dst, const std::vector<float4> &src) -> bool {
+        HIP_TRY(hipMalloc(&dst, std::max<size_t>(16, src.size() * sizeof(float4))));
+        if (!src.empty()) HIP_TRY(hipMemcpy(dst, src.data(), src.size() * sizeof(float4), hipMemcpyHostToDevice));
+        return true;
+    };
+    if (!up(c.nodes, s.scene.nodes) || !up(c.tris, s.scene.tris) || !up(c.shade, s.scene.shade) ||
+        !up(c.albedo, s.scene.albedo))
+        return false;
+    c.sceneVersion = s.scene.version;
+    return true;
+}
+
+bool init_inner(int width, int height, const char **err) {
+    State &s = S();
+    destroy_all();
+    if (width <= 0 || height <= 0) return fail(err, "invalid image size");
+    s.width = width;
+    s.height = height;
+    std::vector<int> devs = s.devices;
+    if (devs.empty()) {
+        int d = 0;
+        HIP_TRY(hipGetDevice(&d));
+        devs.push_back(d);
+    }
+    const int ry0 = std::clamp(s.rowY0, 0, height);
+    const int ry1 = s.rowY1 <= 0 ? height : std::clamp(s.rowY1, ry0, height);
+    const int rows = ry1 - ry0;
+    const int n = int(devs.size());
+    s.ctxs.resize(size_t(n));
+    for (int k = 0; k < n; ++k) {
+        Ctx &c = s.ctxs[size_t(k)];
+        c.device = devs[size_t(k)];
+        c.y0 = ry0 + int((long long)rows * k / n);
+        c.y1 = ry0 + int((long long)rows * (k + 1) / n);
+        HIP_TRY(hipSetDevice(c.device));
+        HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
+        const size_t px = size_t(c.y1 - c.y0) * size_t(width);
+        HIP_TRY(hipMalloc(&c.accum, std::max<size_t>(16, px * sizeof(float4))));
+        HIP_TRY(hipMalloc(&c.out, std::max<size_t>(16, px * sizeof(uint32_t))));
+        HIP_TRY(hipMalloc(&c.queue, 64));
+        HIP_TRY(hipMalloc(&c.stats, 64));
+        HIP_TRY(hipMemsetAsync(c.accum, 0, px * sizeof(float4), c.stream));
+        HIP_TRY(hipMemsetAsync(c.out, 0, px * sizeof(uint32_t), c.stream));
+        HIP_TRY(hipMemsetAsync(c.stats, 0, 64, c.stream));
+        HIP_TRY(hipDeviceGetAttribute(&c.cus, hipDeviceAttributeMultiprocessorCount, c.device));
+        c.meshBlocksPerCu[0] = hippt::mesh_blocks_per_cu(false);
+        c.meshBlocksPerCu[1] = hippt::mesh_blocks_per_cu(true);
+        HIP_TRY(hipStreamSynchronize(c.stream));
+    }
+    s.hostCount = size_t(width) * size_t(height);
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.host), s.hostCount * sizeof(unsigned), hipHostMallocPortable));
+    std::memset(s.host, 0, s.hostCount * sizeof(unsigned));
+    s.ready = true;
+    return true;
+}
+
+// Cleans up on failure, as cudaPathTracerInit does (CudaPathTracerKernel.cu:202-234).
+bool init_locked(int width, int height, const char **err) {
+    if (init_inner(width, height, err)) return true;
+    destroy_all();
+    return false;
+}
+
+CameraF current_camera() {
+    State &s = S();
+    if (s.scene.rawCamera) return s.scene.cam;
+    CameraF cam;
+    build_camera(s.scene.lookfrom, s.scene.lookat, s.scene.vup, s.scene.vfov, double(s.width) / double(s.height),
+                 s.scene.aperture, s.scene.focus, cam);
+    return cam;
+}
+
+// Enqueues `count` frames on every context (no host wait).
+bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const char **err) {
+    State &s = S();
+    if (!s.ready) return fail(err, "HIP path tracer not initialized");
+    if (count < 0) return fail(err, "negative frame count");
+    const bool mesh = s.scene.kind == HIPPT_SCENE_MESH;
+    const CameraF cam = mesh ? current_camera() : CameraF{};
+    for (Ctx &c : s.ctxs) {
+        HIP_TRY(hipSetDevice(c.device));
+        const int rows = c.y1 - c.y0;
+        const unsigned bandPixels = unsigned(rows) * unsigned(s.width);
+        if (rows > 0 && count > 0) {
+            if (!mesh) {
+                hippt::Sphere4Params p{c.accum, c.out, c.stats, s.width, s.height, c.y0, rows, firstFrame, count, maxDepth};
+                EventPair ev;
+                if (!next_events(c, ev, err)) return false;
+                HIP_TRY(hipEventRecord(ev.a, c.stream));
+                HIP_TRY(hippt::launch_sphere4(p, c.stream));
+                HIP_TRY(hipEventRecord(ev.b, c.stream));
+                c.pending.push_back({0, ev});
+            } else {
+                if (!ensure_scene(c, err)) return false;
+                const size_t perFrame = size_t(bandPixels) * 3 * sizeof(float);
+                const size_t cap = size_t(std::max<long long>(1, s.scratchMB)) << 20;
+                int fpb = int(std::max<size_t>(1, cap / perFrame));
+                fpb = std::min(fpb, count);
+                fpb = int(std::min<long long>(fpb, (1LL << 31) / std::max<unsigned>(1, bandPixels)));
+                fpb = std::max(fpb, 1);
+                const size_t need = perFrame * size_t(fpb);
+                if (c.scratchBytes < need) {
+                    HIP_TRY(hipStreamSynchronize(c.stream));
+                    (void)hipFree(c.scratch);
+                    c.scratch = nullptr;
+                    c.scratchBytes = 0;
+                    HIP_TRY(hipMalloc(&c.scratch, need));
+                    c.scratchBytes = need;
+                }
+                const bool cnt = s.countTraversal;
+                int bpc = s.blocksPerCu > 0 ? s.blocksPerCu : c.meshBlocksPerCu[cnt ? 1 : 0];
+                for (int b = 0; b < count; b += fpb) {
+                    const int nf = std::min(fpb, count - b);
+                    const unsigned total = bandPixels * unsigned(nf);
+                    if (maxDepth <= 0) {
+                        // ray_color with depth <= 0 returns black without tracing (RayTracer.h:582-583)
+                        HIP_TRY(hipMemsetAsync(c.scratch, 0, size_t(total) * 3 * sizeof(float), c.stream));
+                    } else {
+                        hippt::MeshParams p{};
+                        p.nodes = c.nodes;
+                        p.tris = c.tris;
+                        p.shade = c.shade;
+                        p.albedo = c.albedo;
+                        p.scratch = c.scratch;
+                        p.queue = c.queue;
+                        p.stats = c.stats;
+                        p.cam = cam;
+                        p.invW = 1.0f / float(std::max(1, s.width - 1));
+                        p.invH = 1.0f / float(std::max(1, s.height - 1));
+                        p.width = s.width;
+                        p.height = s.height;
+                        p.y0 = c.y0;
+                        p.bandRows = rows;
+                        p.firstFrame = firstFrame + b;
+                        p.frames = nf;
+                        p.maxDepth = maxDepth;
+                        p.bandPixels = bandPixels;
+                        p.totalItems = total;
+                        p.waveThreshold = s.waveThreshold;
+                        p.chunk = s.chunk;
+                        long long blocks = (long long)c.cus * bpc;
+                        blocks = std::min<long long>(blocks, (total + hippt::kMeshBlock - 1) / hippt::kMeshBlock);
+                        blocks = std::max<long long>(blocks, 1);
+                        HIP_TRY(hipMemsetAsync(c.queue, 0, sizeof(unsigned), c.stream));
+                        EventPair ev;
+                        if (!next_events(c, ev, err)) return false;
+                        HIP_TRY(hipEventRecord(ev.a, c.stream));
+                        HIP_TRY(hippt::launch_mesh(p, int(blocks), cnt, c.stream));
+                        HIP_TRY(hipEventRecord(ev.b, c.stream));
+                        c.pending.push_back({0, ev});
+                    }
+                    hippt::CombineParams q{c.accum, c.out, c.scratch, bandPixels, total, firstFrame + b, nf};
+                    EventPair ev2;
+                    if (!next_events(c, ev2, err)) return false;
+                    HIP_TRY(hipEventRecord(ev2.a, c.stream));
+                    HIP_TRY(hippt::launch_combine(q, c.stream));
+                    HIP_TRY(hipEventRecord(ev2.b, c.stream));
+                    c.pending.push_back({1, ev2});
+                }
+            }
+        }
+        if (copy && rows > 0) {
+            HIP_TRY(hipMemcpyAsync(s.host + size_t(c.y0) * size_t(s.width), c.out, size_t(bandPixels) * sizeof(uint32_t),
+                                   hipMemcpyDeviceToHost, c.stream));
+        }
+    }
+    return true;
+}
+
+bool sync_locked(const char **err) {
+    State &s = S();
+    for (Ctx &c : s.ctxs) {
+        HIP_TRY(hipSetDevice(c.device));
+        HIP_TRY(hipStreamSynchronize(c.stream));
+        for (auto &pe : c.pending) {
+            float ms = 0.0f;
+            HIP_TRY(hipEventElapsedTime(&ms, pe.second.a, pe.second.b));
+            if (pe.first == 0) {
+                s.traceMs += ms;
+                ++s.traceLaunches;
+            } else {
+                s.combineMs += ms;
+                ++s.combineLaunches;
+            }
+        }
+        c.pending.clear();
+        c.poolUsed = 0;
+    }
+    return true;
+}
+
+bool render_locked(int frameIndex, int count, int maxDepth, const unsigned int **hostPixels, const char **err) {
+    if (!enqueue_locked(frameIndex, count, maxDepth, true, err)) return false;
+    if (!sync_locked(err)) return false;
+    if (hostPixels) *hostPixels = S().host;
+    return true;
+}
+
+}  // namespace
+
+// ---- reference ABI ----------------------------------------------------------------------------
+extern "C" bool cudaPathTracerInit(int width, int height, const char **errorMessage) {
+    std::lock_guard<std::mutex> g(S().mu);
+    return init_locked(width, height, errorMessage);
+}
+
+extern "C" bool cudaPathTracerRender(int frameIndex, int maxDepth, const unsigned int **hostPixels,
+                                     const char **errorMessage) {
+    std::lock_guard<std::mutex> g(S().mu);
+    return render_locked(frameIndex, 1, maxDepth, hostPixels, errorMessage);
+}
+
+extern "C" void cudaPathTracerShutdown(void) {
+    std::lock_guard<std::mutex> g(S().mu);
+    destroy_all();
+}
+
+extern "C" bool hipPathTracerInit(int width, int height, const char **errorMessage) {
+    return cudaPathTracerInit(width, height, errorMessage);
+}
+extern "C" bool hipPathTracerRender(int frameIndex, int maxDepth, const unsigned int **hostPixels,
+                                    const char **errorMessage) {
+    return cudaPathTracerRender(frameIndex, maxDepth, hostPixels, errorMessage);
+}
+extern "C" void hipPathTracerShutdown(void) { cudaPathTracerShutdown(); }
+
+// ---- scene --------------------------------------------------------------------------------------
+extern "C" void hipptBuildCamera(const double lookfrom[3], const double lookat[3], const double vup[3],
+                                 double vfovDeg, double aspect, double aperture, double focusDist, hipptCamera *out) {
+    static_assert(sizeof(hipptCamera) == sizeof(CameraF), "camera layout");
+    CameraF c;
+    build_camera(lookfrom, lookat, vup, vfovDeg, aspect, aperture, focusDist, c);
+    std::memcpy(out, &c, sizeof(c));
+}
+
+extern "C" bool hipptUseBuiltinScene(int sceneId, const char **err) {
+    std::lock_guard<std::mutex> g(S().mu);
+    if (sceneId != HIPPT_SCENE_SPHERE4) return fail(err, "unknown built-in scene id");
+    S().scene.kind = HIPPT_SCENE_SPHERE4;
+    return true;
+}
+
+extern "C" bool hipptUploadMesh(const float *verts, const int *triMaterial, int numTris, const float *albedo,
+                                int numMaterials, const double lookfrom[3], const double lookat[3],
+                                const double vup[3], double vfovDeg, double aperture, double focusDist,
+                                const char **err) {
+    std::lock_guard<std::mutex> g(S().mu);
+    State &s = S();
+    if (!verts || !triMaterial || !albedo || !lookfrom || !lookat || !vup) return fail(err, "null scene pointer");
+    if (numMaterials <= 0) return fail(err, "scene needs at least one material");
+    for (int i = 0; i < numTris; ++i)
+        if (triMaterial[i] < 0 || triMaterial[i] >= numMaterials) return fail(err, "triangle material out of range");
+    float extent = 0.0f;
+    for (int i = 0; i < 3; ++i) extent = std::max(extent, float(std::fabs(lookfrom[i])));
+    hippt::Bvh bvh;
+    std::string msg;
+    if (!hippt::build_bvh(verts, numTris, extent, bvh, msg)) return fail(err, msg);
+    SceneHost &sc = s.scene;
+    sc.nodes.assign(bvh.nodes.size() / 4, float4{});
+    std::memcpy(sc.nodes.data(), bvh.nodes.data(), bvh.nodes.size() * sizeof(uint32_t));
+    sc.tris.assign(size_t(numTris) * 3, float4{});
+    sc.shade.assign(size_t(numTris), float4{});
+    for (int k = 0; k < numTris; ++k) {
+        const int id = bvh.order[size_t(k)];
+        const float *v = verts + 9 * size_t(id);
+        // po_tri_setup (oracle) restated: e1 = v1-v0, e2 = v2-v0, n = cross/len
+        float e1[3] = {v[3] - v[0], v[4] - v[1], v[5] - v[2]};
+        float e2[3] = {v[6] - v[0], v[7] - v[1], v[8] - v[2]};
+        float cr[3], n[3];
+        fcross(e1, e2, cr);
+        const float len = std::sqrt(fdot(cr, cr));
+        if (!(len > 0.0f)) {
+            e1[0] = e1[1] = e1[2] = 0.0f;
+            e2[0] = e2[1] = e2[2] = 0.0f;
+            n[0] = n[1] = n[2] = 0.0f;
+        } else {
+            const float inv = 1.0f / len;
+            for (int a = 0; a < 3; ++a) n[a] = cr[a] * inv;
+        }
+        sc.tris[3 * size_t(k)] = float4{v[0], v[1], v[2], e1[0]};
+        sc.tris[3 * size_t(k) + 1] = float4{e1[1], e1[2], e2[0], e2[1]};
+        sc.tris[3 * size_t(k) + 2] = float4{e2[2], as_float(id), 0.0f, 0.0f};
+        sc.shade[size_t(k)] = float4{n[0], n[1], n[2], as_float(triMaterial[id])};
+    }
+    sc.albedo.assign(size_t(numMaterials), float4{});
+    for (int m = 0; m < numMaterials; ++m)
+        sc.albedo[size_t(m)] = float4{albedo[3 * m], albedo[3 * m + 1], albedo[3 * m + 2], 0.0f};
+    sc.numTris = numTris;
+    sc.numNodes = int(bvh.nodes.size() / hippt::kNodeWords);
+    sc.levels = bvh.levels;
+    for (int i = 0; i < 3; ++i) {
+        sc.lookfrom[i] = lookfrom[i];
+        sc.lookat[i] = lookat[i];
+        sc.vup[i] = vup[i];
+    }
+    sc.vfov = vfovDeg;
+    sc.aperture = aperture;
+    sc.focus = focusDist;
+    sc.rawCamera = false;
+    sc.kind = HIPPT_SCENE_MESH;
+    ++sc.version;
+    return true;
+}
+
+extern "C" bool hipptSetCamera(const hipptCamera *camera, const char **err) {
+    std::lock_guard<std::mutex> g(S().mu);
+    if (!camera) return fail(err, "null camera");
+    std::memcpy(&S().scene.cam, camera, sizeof(CameraF));
+    S().scene.rawCamera = true;
+    return true;
+}
+
+// ---- devices ------------------------------------------------------------------------------------
+extern "C" int hipptDeviceCount(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+extern "C" bool hipptSetDevices(const int *deviceIds, int numDevices, const char **err) {
+    std::lock_guard<std::mutex> g(S().mu);
+    State &s = S();
+    if (numDevices < 0 || (numDevices > 0 && !deviceIds)) return fail(err, "invalid device list");
+    int avail = 0;
+    HIP_TRY(hipGetDeviceCount(&avail));
+    for (int i = 0; i < numDevices; ++i)
+        if (deviceIds[i] < 0 || deviceIds[i] >= avail) return fail(err, "device id out of range");
+    s.devices.assign(deviceIds, deviceIds + numDevices);
+    return true;
+}
+
+extern "C" bool hipptSetRowRange(int y0, int y1, const char **err) {
+    std::lock_guard<std::mutex> g(S().mu);
+    if (y0 < 0 || (y1 > 0 && y1 < y0)) return fail(err, "invalid row range");
+    S().rowY0 = y0;
+    S().rowY1 = y1;
+    return true;
+}
+
+// ---- rendering ----------------------------------------------------------------------------------
+extern "C" bool hipptRenderFrames(int firstFrame, int count, int maxDepth, const unsigned int **hostPixels,
+                                  const char **err) {
+    std::lock_guard<std::mutex> g(S().mu);
+    return render_locked(firstFrame, count, maxDepth, hostPixels, err);
+}
+
+extern "C" bool hipptRenderFramesAsync(int firstFrame, int count, int maxDepth, const char **err) {
+    std::lock_guard<std::mutex> g(S().mu);
+    return enqueue_locked(firstFrame, count, maxDepth, false, err);
+}
+
+extern "C" bool hipptSynchronize(const char **err) {
+    std::lock_guard<std::mutex> g(S().mu);
+    return sync_locked(err);
+}
+
+extern "C" bool hipptReadback(unsigned int *pixels, float *accum, const char **err) {
+    std::lock_guard<std::mutex> g(S().mu);
+    State &s = S();
+    if (!s.ready) return fail(err, "HIP path tracer not initialized");
+    if (!sync_locked(err)) return false;
+    for (Ctx &c : s.ctxs) {
+        HIP_TRY(hipSetDevice(c.device));
+        const size_t px = size_t(c.y1 - c.y0) * size_t(s.width);
+        if (px == 0) continue;
+        if (pixels)
+            HIP_TRY(hipMemcpy(pixels + size_t(c.y0) * s.width, c.out, px * sizeof(uint32_t), hipMemcpyDeviceToHost));
+        if (accum)
+            HIP_TRY(hipMemcpy(accum + size_t(c.y0) * s.width * 4, c.accum, px * sizeof(float4), hipMemcpyDeviceToHost));
+    }
+    return true;
+}
+
+extern "C" bool hipptResetAccumulation(const char **err) {
+    std::lock_guard<std::mutex> g(S().mu);
+    State &s = S();
+    if (!s.ready) return fail(err, "HIP path tracer not initialized");
+    for (Ctx &c : s.ctxs) {
+        HIP_TRY(hipSetDevice(c.device));
+        const size_t px = size_t(c.y1 - c.y0) * size_t(s.width);
+        HIP_TRY(hipMemsetAsync(c.accum, 0, px * sizeof(float4), c.stream));
+        HIP_TRY(hipStreamSynchronize(c.stream));
+    }
+    return true;
+}
+
+// ---- counters / options -------------------------------------------------------------------------
+extern "C" bool hipptGetStats(hipptStats *out) {
+    std::lock_guard<std::mutex> g(S().mu);
+    State &s = S();
+    if (!out) return false;
+    std::memset(out, 0, sizeof(*out));
+    const char *err = nullptr;
+    if (s.ready && !sync_locked(&err)) return false;
+    for (Ctx &c : s.ctxs) {
+        unsigned long long v[4] = {0, 0, 0, 0};
+        if (hipSetDevice(c.device) != hipSuccess) return false;
+        if (hipMemcpy(v, c.stats, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return false;
+        out->segments += v[0];
+        out->pixelSamples += v[1];
+        out->nodeVisits += v[2];
+        out->triTests += v[3];
+    }
+    out->traceMs = s.traceMs;
+    out->combineMs = s.combineMs;
+    out->traceLaunches = s.traceLaunches;
+    out->combineLaunches = s.combineLaunches;
+    out->bvhNodes = s.scene.kind == HIPPT_SCENE_MESH ? s.scene.numNodes : 0;
+    out->bvhDepth = s.scene.kind == HIPPT_SCENE_MESH ? s.scene.levels : 0;
+    out->numTris = s.scene.kind == HIPPT_SCENE_MESH ? s.scene.numTris : 0;
+    out->numDevices = int(s.ctxs.size());
+    return true;
+}
+
+extern "C" void hipptResetStats(void) {
+    std::lock_guard<std::mutex> g(S().mu);
+    State &s = S();
+    const char *err = nullptr;
+    if (s.ready) sync_locked(&err);
+    for (Ctx &c : s.ctxs) {
+        (void)hipSetDevice(c.device);
+        (void)hipMemset(c.stats, 0, 64);
+    }
+    s.traceMs = s.combineMs = 0;
+    s.traceLaunches = s.combineLaunches = 0;
+}
+
+extern "C" bool hipptSetOption(int key, long long value) {
+    std::lock_guard<std::mutex> g(S().mu);
+    State &s = S();
+    switch (key) {
+    case HIPPT_OPT_COUNT_TRAVERSAL: s.countTraversal = value != 0; return true;
+    case HIPPT_OPT_WAVE_THRESHOLD:
+        if (value < 0 || value > 64) return false;
+        s.waveThreshold = int(value);
+        return true;
+    case HIPPT_OPT_SCRATCH_MB:
+        if (value < 1) return false;
+        s.scratchMB = value;
+        return true;
+    case HIPPT_OPT_CHUNK:
+        if (value < 64 || value > (1 << 20) || value % 64) return false;
+        s.chunk = unsigned(value);
+        return true;
+    case HIPPT_OPT_BLOCKS_PER_CU:
+        if (value < 0 || value > 8) return false;
+        s.blocksPerCu = int(value);
+        return true;
+    default: return false;
+    }
+}
+
+extern "C" long long hipptGetOption(int key) {
+    std::lock_guard<std::mutex> g(S().mu);
+    State &s = S();
+    switch (key) {
+    case HIPPT_OPT_COUNT_TRAVERSAL: return s.countTraversal ? 1 : 0;
+    case HIPPT_OPT_WAVE_THRESHOLD: return s.waveThreshold;
+    case HIPPT_OPT_SCRATCH_MB: return s.scratchMB;
+    case HIPPT_OPT_CHUNK: return s.chunk;
+    case HIPPT_OPT_BLOCKS_PER_CU: return s.blocksPerCu;
+    default: return -1;
+    }
+}
+
+extern "C" const char *hipptLastError(void) { return S().error; }
+
+// ---- host BVH builder -----------------------------------------------------------------------------
+extern "C" hipptBvh *hipptBvhBuild(const float *verts, int numTris, float extentHint, const char **err) {
+    auto *b = new hipptBvh();
+    std::string msg;
+    if (!verts || !hippt::build_bvh(verts, numTris, extentHint, b->bvh, msg)) {
+        delete b;
+        std::lock_guard<std::mutex> g(S().mu);
+        fail(err, msg.empty() ? "null vertex pointer" : msg);
+        return nullptr;
+    }
+    return b;
+}
+
+extern "C" int hipptBvhNodeCount(const hipptBvh *b) { return b ? int(b->bvh.nodes.size() / hippt::kNodeWords) : 0; }
+extern "C" int hipptBvhDepth(const hipptBvh *b) { return b ? b->bvh.levels : 0; }
+extern "C" void hipptBvhCopy(const hipptBvh *b, uint32_t *nodes, int *triOrder) {
+    if (!b) return;
+    if (nodes) std::memcpy(nodes, b->bvh.nodes.data(), b->bvh.nodes.size() * sizeof(uint32_t));
+    if (triOrder) std::memcpy(triOrder, b->bvh.order.data(), b->bvh.order.size() * sizeof(int));
+}
+extern "C" void hipptBvhFree(hipptBvh *b) { delete b; }

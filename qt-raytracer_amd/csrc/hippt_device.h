@@ -1,0 +1,62 @@
+// hippt_device.h — launch parameter blocks shared by the host API (hippt_api.cpp) and the
+// gfx950 kernels (hippt_kernels.hip).  Plain structs passed by value as kernel arguments.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace hippt {
+
+struct CameraF {  // layout == hipptCamera (include/hippt.h)
+    float origin[3], llc[3], horizontal[3], vertical[3], u[3], v[3];
+    float lens_radius;
+    float reserved;
+};
+
+// Legacy 4-sphere scene (CudaPathTracerKernel.cu:136-179), rows [y0, y0+rows).
+struct Sphere4Params {
+    float4 *accum;      // rows*width RGBA
+    uint32_t *out;      // rows*width ARGB
+    unsigned long long *stats;
+    int width, height, y0, rows;
+    int firstFrame, frames, maxDepth;
+};
+
+// Triangle-mesh megakernel: one persistent grid drains `totalItems` (pixel, frame)
+// samples of rows [y0, y0+bandRows) and frames [firstFrame, firstFrame+frames).
+struct MeshParams {
+    const float4 *nodes;   // 4 float4 per interior node (bvh_builder.h layout)
+    const float4 *tris;    // 3 float4 per triangle: (v0, e1.x) (e1.yz, e2.xy) (e2.z, orig, -, -)
+    const float4 *shade;   // 1 float4 per triangle: unit normal xyz, material index (int bits)
+    const float4 *albedo;  // 1 float4 per material
+    float *scratch;        // 3 planes (R, G, B) of totalItems floats: per-sample radiance
+    unsigned *queue;       // global work counter (zeroed before launch)
+    unsigned long long *stats;  // [0] segments, [1] pixel samples, [2] node visits, [3] tri tests
+    CameraF cam;
+    float invW, invH;      // 1/max(1,W-1), 1/max(1,H-1) (RayTracerFboItem.cpp:61-64)
+    int width, height, y0, bandRows;
+    int firstFrame, frames, maxDepth;
+    unsigned bandPixels, totalItems;
+    int waveThreshold;     // shade once fewer than this many lanes still traverse
+    unsigned chunk;        // items per queue grab (multiple of 64)
+};
+
+// Running average + tonemap over a batch of per-sample radiances
+// (CudaPathTracerKernel.cu:157-178).
+struct CombineParams {
+    float4 *accum;
+    uint32_t *out;
+    const float *scratch;
+    unsigned bandPixels, totalItems;
+    int firstFrame, frames;
+};
+
+hipError_t launch_sphere4(const Sphere4Params &p, hipStream_t s);
+hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hipStream_t s);
+hipError_t launch_combine(const CombineParams &p, hipStream_t s);
+// Resident mesh-kernel blocks per CU (occupancy query).
+int mesh_blocks_per_cu(bool countTraversal);
+constexpr int kMeshBlock = 256;
+
+}  // namespace hippt

@@ -1,0 +1,319 @@
+"""Python host mirror of the reference backend interface, over libhippt.so (C ABI).
+
+``PathTracer`` mirrors ``CudaPathTracer`` (CudaPathTracer.h:6-23 / .cpp:14-94): the same
+methods (initialize, renderFrame, hostPixels, frameIndex, lastError), the same frame-index
+bookkeeping (renderFrame passes the current index and increments it after success,
+CudaPathTracer.cpp:41-57) and the same error behaviour (False + lastError()).  Extensions
+(scene upload, batched frames, devices, row bands, counters) wrap the hippt* entry points
+of include/hippt.h.
+
+The product path is libhippt.so only: if it is missing the import fails loudly — there is
+no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import scenes  # noqa: F401  (re-export)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(os.path.dirname(_HERE), "libhippt.so")
+
+SCENE_SPHERE4 = 0
+SCENE_MESH = 1
+
+OPT_COUNT_TRAVERSAL = 1
+OPT_WAVE_THRESHOLD = 2
+OPT_SCRATCH_MB = 3
+OPT_CHUNK = 4
+OPT_BLOCKS_PER_CU = 5
+
+# Every symbol include/hippt.h declares (checked by tests/test_abi_cpu.py).
+EXPORTS = (
+    "cudaPathTracerInit", "cudaPathTracerRender", "cudaPathTracerShutdown",
+    "hipPathTracerInit", "hipPathTracerRender", "hipPathTracerShutdown",
+    "hipptBuildCamera", "hipptUseBuiltinScene", "hipptUploadMesh", "hipptSetCamera",
+    "hipptDeviceCount", "hipptSetDevices", "hipptSetRowRange",
+    "hipptRenderFrames", "hipptRenderFramesAsync", "hipptSynchronize", "hipptReadback",
+    "hipptResetAccumulation", "hipptGetStats", "hipptResetStats", "hipptSetOption", "hipptGetOption",
+    "hipptLastError", "hipptBvhBuild", "hipptBvhNodeCount", "hipptBvhDepth", "hipptBvhCopy", "hipptBvhFree",
+)
+
+
+class HipptError(RuntimeError):
+    pass
+
+
+class Camera(ctypes.Structure):
+    """hipptCamera (include/hippt.h), 80 bytes."""
+    _fields_ = [("origin", ctypes.c_float * 3), ("llc", ctypes.c_float * 3), ("horizontal", ctypes.c_float * 3),
+                ("vertical", ctypes.c_float * 3), ("u", ctypes.c_float * 3), ("v", ctypes.c_float * 3),
+                ("lens_radius", ctypes.c_float), ("reserved", ctypes.c_float)]
+
+    def as_array(self) -> np.ndarray:
+        return np.frombuffer(bytes(self), dtype=np.float32).copy()
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [("segments", ctypes.c_ulonglong), ("pixelSamples", ctypes.c_ulonglong),
+                ("nodeVisits", ctypes.c_ulonglong), ("triTests", ctypes.c_ulonglong),
+                ("traceMs", ctypes.c_double), ("combineMs", ctypes.c_double),
+                ("traceLaunches", ctypes.c_int), ("combineLaunches", ctypes.c_int),
+                ("bvhNodes", ctypes.c_int), ("bvhDepth", ctypes.c_int), ("numTris", ctypes.c_int),
+                ("numDevices", ctypes.c_int)]
+
+    def as_dict(self) -> dict:
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Loads libhippt.so and declares the C signatures.  Raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise HipptError(f"{path} is missing: build it with `make -C qt-raytracer_amd` "
+                         "(or __graft_entry__.build()); there is no fallback path")
+    lib = ctypes.CDLL(path)
+    c_int, c_bool, c_char_p, c_double, c_float = ctypes.c_int, ctypes.c_bool, ctypes.c_char_p, ctypes.c_double, ctypes.c_float
+    pp_char = ctypes.POINTER(ctypes.c_char_p)
+    p_uint = ctypes.POINTER(ctypes.c_uint)
+    pp_uint = ctypes.POINTER(p_uint)
+    p_float = ctypes.POINTER(ctypes.c_float)
+    p_int = ctypes.POINTER(ctypes.c_int)
+    p_double = ctypes.POINTER(ctypes.c_double)
+
+    def sig(name, res, *args):
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = list(args)
+
+    for pre in ("cuda", "hip"):
+        sig(f"{pre}PathTracerInit", c_bool, c_int, c_int, pp_char)
+        sig(f"{pre}PathTracerRender", c_bool, c_int, c_int, pp_uint, pp_char)
+        sig(f"{pre}PathTracerShutdown", None)
+    sig("hipptBuildCamera", None, p_double, p_double, p_double, c_double, c_double, c_double, c_double,
+        ctypes.POINTER(Camera))
+    sig("hipptUseBuiltinScene", c_bool, c_int, pp_char)
+    sig("hipptUploadMesh", c_bool, p_float, p_int, c_int, p_float, c_int, p_double, p_double, p_double,
+        c_double, c_double, c_double, pp_char)
+    sig("hipptSetCamera", c_bool, ctypes.POINTER(Camera), pp_char)
+    sig("hipptDeviceCount", c_int)
+    sig("hipptSetDevices", c_bool, p_int, c_int, pp_char)
+    sig("hipptSetRowRange", c_bool, c_int, c_int, pp_char)
+    sig("hipptRenderFrames", c_bool, c_int, c_int, c_int, pp_uint, pp_char)
+    sig("hipptRenderFramesAsync", c_bool, c_int, c_int, c_int, pp_char)
+    sig("hipptSynchronize", c_bool, pp_char)
+    sig("hipptReadback", c_bool, p_uint, p_float, pp_char)
+    sig("hipptResetAccumulation", c_bool, pp_char)
+    sig("hipptGetStats", c_bool, ctypes.POINTER(Stats))
+    sig("hipptResetStats", None)
+    sig("hipptSetOption", c_bool, c_int, ctypes.c_longlong)
+    sig("hipptGetOption", ctypes.c_longlong, c_int)
+    sig("hipptLastError", c_char_p)
+    sig("hipptBvhBuild", ctypes.c_void_p, p_float, c_int, c_float, pp_char)
+    sig("hipptBvhNodeCount", c_int, ctypes.c_void_p)
+    sig("hipptBvhDepth", c_int, ctypes.c_void_p)
+    sig("hipptBvhCopy", None, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), p_int)
+    sig("hipptBvhFree", None, ctypes.c_void_p)
+    _lib = lib
+    return lib
+
+
+def _err(e: ctypes.c_char_p, default: str) -> str:
+    return e.value.decode() if e.value else default
+
+
+def _ptr(a: np.ndarray, ct):
+    return a.ctypes.data_as(ctypes.POINTER(ct))
+
+
+def _d3(v) -> ctypes.Array:
+    return (ctypes.c_double * 3)(*[float(x) for x in v])
+
+
+def build_camera(lookfrom, lookat, vup, vfov, aspect, aperture, focus) -> Camera:
+    lib = load_library()
+    cam = Camera()
+    lib.hipptBuildCamera(_d3(lookfrom), _d3(lookat), _d3(vup), float(vfov), float(aspect), float(aperture),
+                         float(focus), ctypes.byref(cam))
+    return cam
+
+
+class Bvh:
+    """Host BVH built by libhippt (hipptBvhBuild): nodes (N,16) uint32 and triangle order."""
+
+    def __init__(self, verts: np.ndarray, extent_hint: float = 0.0):
+        lib = load_library()
+        v = np.ascontiguousarray(verts, dtype=np.float32).reshape(-1, 9)
+        e = ctypes.c_char_p()
+        h = lib.hipptBvhBuild(_ptr(v, ctypes.c_float), int(v.shape[0]), float(extent_hint), ctypes.byref(e))
+        if not h:
+            raise HipptError(_err(e, "BVH build failed"))
+        try:
+            n = lib.hipptBvhNodeCount(h)
+            self.depth = lib.hipptBvhDepth(h)
+            self.nodes = np.zeros((n, 16), dtype=np.uint32)
+            self.order = np.zeros(v.shape[0], dtype=np.int32)
+            lib.hipptBvhCopy(h, _ptr(self.nodes, ctypes.c_uint32), _ptr(self.order, ctypes.c_int))
+        finally:
+            lib.hipptBvhFree(h)
+
+
+class PathTracer:
+    """Mirror of CudaPathTracer (CudaPathTracer.h:6-23) over the HIP backend."""
+
+    def __init__(self):
+        self._lib = load_library()
+        self._width = 0
+        self._height = 0
+        self._frame_index = 0
+        self._pixels: Optional[ctypes.POINTER] = None
+        self._last_error = ""
+
+    def __del__(self):  # ~CudaPathTracer -> cudaPathTracerShutdown (CudaPathTracer.cpp:14-18)
+        try:
+            self._lib.cudaPathTracerShutdown()
+        except Exception:
+            pass
+
+    # --- CudaPathTracer interface -------------------------------------------------------------
+    def initialize(self, width: int, height: int) -> bool:
+        self._width, self._height = int(width), int(height)
+        self._frame_index = 0
+        self._pixels = None
+        e = ctypes.c_char_p()
+        if not self._lib.cudaPathTracerInit(self._width, self._height, ctypes.byref(e)):
+            self._last_error = _err(e, "HIP initialization failed")
+            return False
+        return True
+
+    def renderFrame(self, maxDepth: int) -> bool:  # noqa: N802 (reference name)
+        e = ctypes.c_char_p()
+        px = ctypes.POINTER(ctypes.c_uint)()
+        if not self._lib.cudaPathTracerRender(self._frame_index, int(maxDepth), ctypes.byref(px), ctypes.byref(e)):
+            self._last_error = _err(e, "HIP render failed")
+            return False
+        self._pixels = px
+        self._frame_index += 1
+        return True
+
+    def hostPixels(self) -> Optional[np.ndarray]:  # noqa: N802
+        """Copy of the library-owned W*H ARGB frame (row 0 = v = 0), or None before a render."""
+        if not self._pixels:
+            return None
+        n = self._width * self._height
+        return np.ctypeslib.as_array(self._pixels, shape=(n,)).reshape(self._height, self._width).copy()
+
+    def frameIndex(self) -> int:  # noqa: N802
+        return self._frame_index
+
+    def lastError(self) -> str:  # noqa: N802
+        return self._last_error
+
+    # --- GpuPathTracer-shaped extensions (GpuPathTracer.h:9-38) -------------------------------
+    def renderFrames(self, samplesPerFrame: int, maxDepth: int, copy: bool = True) -> bool:  # noqa: N802
+        """Renders samplesPerFrame frames at once, continuing the frame index."""
+        e = ctypes.c_char_p()
+        px = ctypes.POINTER(ctypes.c_uint)()
+        ok = self._lib.hipptRenderFrames(self._frame_index, int(samplesPerFrame), int(maxDepth),
+                                         ctypes.byref(px) if copy else None, ctypes.byref(e))
+        if not ok:
+            self._last_error = _err(e, "HIP render failed")
+            return False
+        if copy:
+            self._pixels = px
+        self._frame_index += int(samplesPerFrame)
+        return True
+
+    def renderFramesAsync(self, samplesPerFrame: int, maxDepth: int) -> bool:  # noqa: N802
+        e = ctypes.c_char_p()
+        if not self._lib.hipptRenderFramesAsync(self._frame_index, int(samplesPerFrame), int(maxDepth), ctypes.byref(e)):
+            self._last_error = _err(e, "HIP render failed")
+            return False
+        self._frame_index += int(samplesPerFrame)
+        return True
+
+    def synchronize(self) -> bool:
+        e = ctypes.c_char_p()
+        if not self._lib.hipptSynchronize(ctypes.byref(e)):
+            self._last_error = _err(e, "HIP synchronize failed")
+            return False
+        return True
+
+    def resetAccumulation(self) -> bool:  # noqa: N802
+        e = ctypes.c_char_p()
+        if not self._lib.hipptResetAccumulation(ctypes.byref(e)):
+            self._last_error = _err(e, "reset failed")
+            return False
+        self._frame_index = 0
+        return True
+
+    def readback(self, y0: int = 0, y1: Optional[int] = None):
+        """(pixels (H,W) uint32, accum (H,W,4) float32) of the current image; rows outside this
+        process's row range are zero."""
+        pixels = np.zeros((self._height, self._width), dtype=np.uint32)
+        accum = np.zeros((self._height, self._width, 4), dtype=np.float32)
+        e = ctypes.c_char_p()
+        if not self._lib.hipptReadback(_ptr(pixels, ctypes.c_uint), _ptr(accum, ctypes.c_float), ctypes.byref(e)):
+            raise HipptError(_err(e, "readback failed"))
+        y1 = self._height if y1 is None else y1
+        return pixels[y0:y1], accum[y0:y1]
+
+    # --- scene / devices / counters -------------------------------------------------------------
+    def useBuiltinScene(self, scene_id: int = SCENE_SPHERE4) -> None:  # noqa: N802
+        e = ctypes.c_char_p()
+        if not self._lib.hipptUseBuiltinScene(int(scene_id), ctypes.byref(e)):
+            raise HipptError(_err(e, "bad scene"))
+
+    def uploadMesh(self, scene) -> None:  # noqa: N802
+        v = np.ascontiguousarray(scene.verts, dtype=np.float32).reshape(-1, 9)
+        m = np.ascontiguousarray(scene.tri_mat, dtype=np.int32)
+        a = np.ascontiguousarray(scene.albedo, dtype=np.float32).reshape(-1, 3)
+        e = ctypes.c_char_p()
+        ok = self._lib.hipptUploadMesh(_ptr(v, ctypes.c_float), _ptr(m, ctypes.c_int), int(v.shape[0]),
+                                       _ptr(a, ctypes.c_float), int(a.shape[0]), _d3(scene.lookfrom),
+                                       _d3(scene.lookat), _d3(scene.vup), float(scene.vfov),
+                                       float(scene.aperture), float(scene.focus), ctypes.byref(e))
+        if not ok:
+            raise HipptError(_err(e, "mesh upload failed"))
+
+    def setDevices(self, device_ids: Sequence[int]) -> None:  # noqa: N802
+        arr = (ctypes.c_int * max(1, len(device_ids)))(*device_ids)
+        e = ctypes.c_char_p()
+        if not self._lib.hipptSetDevices(arr, len(device_ids), ctypes.byref(e)):
+            raise HipptError(_err(e, "bad devices"))
+
+    def setRowRange(self, y0: int, y1: int) -> None:  # noqa: N802
+        e = ctypes.c_char_p()
+        if not self._lib.hipptSetRowRange(int(y0), int(y1), ctypes.byref(e)):
+            raise HipptError(_err(e, "bad row range"))
+
+    def setOption(self, key: int, value: int) -> None:  # noqa: N802
+        if not self._lib.hipptSetOption(int(key), int(value)):
+            raise HipptError(f"invalid option {key}={value}")
+
+    def stats(self) -> dict:
+        s = Stats()
+        if not self._lib.hipptGetStats(ctypes.byref(s)):
+            raise HipptError("hipptGetStats failed")
+        return s.as_dict()
+
+    def resetStats(self) -> None:  # noqa: N802
+        self._lib.hipptResetStats()
+
+
+def device_count() -> int:
+    return int(load_library().hipptDeviceCount())
+
+
+def row_band(rank: int, world: int, height: int):
+    """Contiguous row band of rank in [0, world): rows [floor(r*H/N), floor((r+1)*H/N))."""
+    return (rank * height) // world, ((rank + 1) * height) // world

@@ -1,0 +1,61 @@
+"""Regenerates the golden fixtures in tests/golden/ from the REFERENCE CPU path tracer.
+
+Run in the development container only (needs /root/reference to build oracle/_ref):
+
+    make -C oracle ref && python tests/golden/make_golden.py
+
+Outputs (committed; data only — inputs and the reference's outputs):
+  ref_functions.json    FP64 outputs of RayTracer.h Sphere::hit, AABB::hit, surrounding_box,
+                        Camera::get_ray (aperture 0), reflect/refract, degrees_to_radians on
+                        seeded inputs, plus BVHNode closest hits (harness Triangle) on cornell34
+  ref_bvh_blob70k.json  BVHNode closest hits on blob70k
+  ref_converge_<scene>_<W>x<H>_<spp>.npy  per-pixel mean (3) and variance (3) of the reference
+                        ray_color radiance, for statistical agreement tests
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [os.path.join(REPO, "qt-raytracer_amd"), os.path.join(REPO, "oracle")]
+
+from hippt import scenes  # noqa: E402
+import pyoracle  # noqa: E402
+
+CONVERGE = [("cornell34", 64, 64, 4096, 8), ("blob70k", 32, 32, 1024, 8)]
+
+
+def main() -> None:
+    if not os.path.exists(pyoracle.REF_HARNESS_STRICT):
+        raise SystemExit("oracle/_ref not built: make -C oracle ref (needs /root/reference)")
+    tmp = tempfile.mkdtemp()
+    paths = {}
+    for name in ("cornell34", "blob70k"):
+        paths[name] = os.path.join(tmp, name + ".scene")
+        scenes.write_scene_file(scenes.get_scene(name), paths[name])
+    out = os.path.join(HERE, "ref_functions.json")
+    subprocess.run([pyoracle.REF_HARNESS_STRICT, "golden", out, paths["cornell34"]], check=True)
+    blob_json = os.path.join(tmp, "blob.json")
+    subprocess.run([pyoracle.REF_HARNESS_STRICT, "golden", blob_json, paths["blob70k"]], check=True)
+    with open(blob_json) as f:
+        blob = json.load(f)
+    with open(os.path.join(HERE, "ref_bvh_blob70k.json"), "w") as f:
+        json.dump({"bvh_closest": blob["bvh_closest"]}, f)
+    for name, w, h, spp, depth in CONVERGE:
+        raw = os.path.join(tmp, f"{name}.f32")
+        subprocess.run([pyoracle.REF_HARNESS, "converge", paths[name], str(w), str(h), str(spp), str(depth), raw,
+                        str(os.cpu_count() or 1)], check=True)
+        img = np.fromfile(raw, dtype=np.float32).reshape(h, w, 6)
+        np.save(os.path.join(HERE, f"ref_converge_{name}_{w}x{h}_{spp}.npy"), img)
+        print(name, "mean radiance", img[..., :3].mean(axis=(0, 1)))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,95 @@
+"""Host-only checks of libhippt.so (no GPU compute): exports, camera, BVH builder, errors."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import hippt
+import pyoracle as po
+from hippt import scenes
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def test_library_exports_every_declared_symbol():
+    header = open(os.path.join(REPO, "include", "hippt.h")).read()
+    declared = set(re.findall(r"\b((?:cuda|hip)PathTracer\w+|hippt[A-Z]\w*)\s*\(", header))
+    out = subprocess.run(["nm", "-D", "--defined-only", hippt.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = {line.split()[-1] for line in out.splitlines() if " T " in line}
+    assert declared, "parsed no declarations"
+    assert declared <= exported, declared - exported
+    assert declared == set(hippt.EXPORTS)
+    lib = hippt.load_library()
+    for name in declared:
+        assert getattr(lib, name)
+
+
+def test_reference_abi_signatures_are_exact():
+    # CudaPathTracer.cpp:4-8 — the caller's extern "C" declarations
+    header = open(os.path.join(REPO, "include", "hippt.h")).read()
+    assert "bool cudaPathTracerInit(int width, int height, const char **errorMessage);" in header
+    assert ("bool cudaPathTracerRender(int frameIndex, int maxDepth, const unsigned int **hostPixels,\n"
+            "                          const char **errorMessage);") in header
+    assert "void cudaPathTracerShutdown(void);" in header
+
+
+def test_render_before_init_fails_with_reference_message():
+    # CudaPathTracerKernel.cu:240-244 — "not initialized" error, no device work
+    lib = hippt.load_library()
+    lib.cudaPathTracerShutdown()
+    e = ctypes.c_char_p()
+    px = ctypes.POINTER(ctypes.c_uint)()
+    assert not lib.cudaPathTracerRender(0, 8, ctypes.byref(px), ctypes.byref(e))
+    assert b"not initialized" in e.value
+    assert not lib.cudaPathTracerRender(0, 8, None, None)  # null out-pointers allowed
+    lib.cudaPathTracerShutdown()
+    lib.cudaPathTracerShutdown()  # idempotent
+
+
+def test_python_mirror_reports_errors_like_cudapathtracer():
+    pt = hippt.PathTracer()
+    assert pt.frameIndex() == 0
+    assert not pt.renderFrame(8)
+    assert "not initialized" in pt.lastError()
+    assert pt.frameIndex() == 0  # not incremented on failure (CudaPathTracer.cpp:45-50)
+    assert pt.hostPixels() is None
+
+
+@pytest.mark.parametrize("aspect", [16 / 9, 1.0, 0.5])
+def test_camera_bitwise_equals_oracle(aspect):
+    for sc in (scenes.cornell34(), scenes.blob70k()):
+        a = hippt.build_camera(sc.lookfrom, sc.lookat, sc.vup, sc.vfov, aspect, sc.aperture, sc.focus).as_array()
+        b = po.camera(sc.lookfrom, sc.lookat, sc.vup, sc.vfov, aspect, sc.aperture, sc.focus).as_array()
+        assert a.tobytes() == b.tobytes()
+    a = hippt.build_camera((13, 2, 3), (0, 0, 0), (0, 1, 0), 20, 1.5, 0.1, 10).as_array()
+    b = po.camera((13, 2, 3), (0, 0, 0), (0, 1, 0), 20, 1.5, 0.1, 10).as_array()
+    assert a.tobytes() == b.tobytes()
+
+
+def test_options_validate():
+    lib = hippt.load_library()
+    assert lib.hipptSetOption(hippt.OPT_WAVE_THRESHOLD, 8)
+    assert lib.hipptGetOption(hippt.OPT_WAVE_THRESHOLD) == 8
+    assert not lib.hipptSetOption(hippt.OPT_WAVE_THRESHOLD, 65)
+    assert not lib.hipptSetOption(hippt.OPT_CHUNK, 100)
+    assert not lib.hipptSetOption(999, 1)
+    assert lib.hipptSetOption(hippt.OPT_WAVE_THRESHOLD, 16)
+
+
+def test_mesh_upload_validates_inputs():
+    pt = hippt.PathTracer()
+    sc = scenes.cornell34()
+    bad = scenes.Scene("bad", sc.verts, sc.tri_mat.copy(), sc.albedo)
+    bad.tri_mat[3] = 7
+    with pytest.raises(hippt.HipptError, match="material"):
+        pt.uploadMesh(bad)
+    empty = scenes.Scene("empty", np.zeros((0, 9), np.float32), np.zeros(0, np.int32), sc.albedo)
+    with pytest.raises(hippt.HipptError, match="at least one triangle"):  # RayTracer.h:398-400
+        pt.uploadMesh(empty)
+
+
+def test_device_count_without_gpu_is_safe():
+    assert hippt.device_count() >= 0

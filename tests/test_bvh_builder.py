@@ -1,0 +1,94 @@
+"""Invariants of the host SAH BVH builder (replaces BVHNode, RayTracer.h:393-429) and
+result-equivalence of BVH traversal with brute force (the oracle's private BVH)."""
+import numpy as np
+import pytest
+
+import hippt
+import pyoracle as po
+from hippt import scenes
+
+
+def _decode(nodes):
+    boxes = nodes[:, :12].view(np.float32).reshape(-1, 2, 2, 3)  # node, child, lo/hi, xyz
+    kids = nodes[:, 12:14].view(np.int32)
+    return boxes, kids
+
+
+def _walk(nodes):
+    boxes, kids = _decode(nodes)
+    leaves, depth = [], 0
+    stack = [(0, 1)]
+    while stack:
+        n, d = stack.pop()
+        depth = max(depth, d)
+        for c in range(2):
+            k = int(kids[n, c])
+            if k >= 0:
+                stack.append((k, d + 1))
+            else:
+                code = ~k
+                leaves.append((code >> 4, code & 15, n, c))
+    return leaves, depth
+
+
+@pytest.mark.parametrize("name", ["cornell34", "blob70k"])
+def test_bvh_covers_every_triangle_once_and_bounds_children(name):
+    sc = scenes.get_scene(name)
+    bvh = hippt.Bvh(sc.verts, extent_hint=800.0)
+    assert sorted(bvh.order.tolist()) == list(range(sc.num_tris))
+    leaves, depth = _walk(bvh.nodes)
+    assert depth == bvh.depth <= 32  # kernel LDS stack depth
+    covered = np.zeros(sc.num_tris, np.int32)
+    boxes, kids = _decode(bvh.nodes)
+    for first, count, n, c in leaves:
+        assert count <= 4
+        covered[first:first + count] += 1
+        lo, hi = boxes[n, c]
+        v = sc.verts[bvh.order[first:first + count]].reshape(-1, 3)
+        if count:
+            assert np.all(v >= lo) and np.all(v <= hi)  # padded box contains its triangles
+    assert np.all(covered == 1)
+    # interior child boxes contain their children's boxes (surrounding_box, RayTracer.h:251-265)
+    for n in range(len(bvh.nodes)):
+        for c in range(2):
+            k = int(kids[n, c])
+            if k >= 0:
+                lo, hi = boxes[n, c]
+                assert np.all(boxes[k, :, 0] >= lo - 1e-3) and np.all(boxes[k, :, 1] <= hi + 1e-3)
+
+
+def test_single_triangle_scene_root_leaf():
+    v = np.array([[0, 0, -1, 1, 0, -1, 0, 1, -1]], np.float32)
+    bvh = hippt.Bvh(v)
+    leaves, depth = _walk(bvh.nodes)
+    assert len(bvh.nodes) == 1 and depth == 1
+    assert sorted((f, c) for f, c, _, _ in leaves) == [(0, 0), (0, 1)]
+
+
+def test_deep_degenerate_input_respects_stack_bound():
+    # 20k coincident-centroid slivers plus a geometric progression that defeats SAH balance
+    rng = np.random.default_rng(1)
+    n = 20000
+    x = np.cumsum(rng.exponential(size=n) ** 4).astype(np.float32)
+    v = np.zeros((n, 9), np.float32)
+    v[:, 0] = x
+    v[:, 3] = x + 1e-3
+    v[:, 7] = 1.0
+    bvh = hippt.Bvh(v)
+    assert bvh.depth <= 32
+    assert sorted(bvh.order.tolist()) == list(range(n))
+
+
+def test_empty_scene_rejected():
+    with pytest.raises(hippt.HipptError):
+        hippt.Bvh(np.zeros((0, 9), np.float32))
+
+
+@pytest.mark.parametrize("name,w,h", [("cornell34", 48, 32), ("blob70k", 24, 16)])
+def test_bvh_traversal_equals_brute_force(name, w, h):
+    sc = scenes.get_scene(name)
+    brute = po.MeshScene(sc, w, h, accel=0)
+    bvh = po.MeshScene(sc, w, h, accel=1)
+    a = brute.frames(0, 2, 8)
+    b = bvh.frames(0, 2, 8)
+    assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]

@@ -1,0 +1,207 @@
+"""GPU parity: libhippt.so on an MI355X vs the CPU oracle (oracle/pt_oracle.c), bit-exact.
+
+Bar: integer/byte outputs (ARGB words, segment counts) identical; accumulation floats
+bit-identical (the arithmetic contract makes every float op the same on both sides).
+All calls go through the C ABI (legacy cudaPathTracer* and hippt* extensions).
+"""
+import numpy as np
+import pytest
+
+import hippt
+import pyoracle as po
+from hippt import scenes
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture()
+def pt():
+    t = hippt.PathTracer()
+    t.setDevices([])
+    t.setRowRange(0, 0)
+    t.useBuiltinScene(hippt.SCENE_SPHERE4)
+    for k, v in ((hippt.OPT_WAVE_THRESHOLD, 16), (hippt.OPT_SCRATCH_MB, 256), (hippt.OPT_CHUNK, 256),
+                 (hippt.OPT_COUNT_TRAVERSAL, 0), (hippt.OPT_BLOCKS_PER_CU, 0)):
+        t.setOption(k, v)
+    t.resetStats()
+    yield t
+    hippt.load_library().cudaPathTracerShutdown()
+
+
+def _assert_same(gpu_px, gpu_acc, ora_px, ora_acc):
+    diff = np.count_nonzero(gpu_px != ora_px)
+    assert diff == 0, f"{diff} of {ora_px.size} pixels differ"
+    assert gpu_acc.tobytes() == ora_acc.tobytes()
+
+
+# ---- legacy 4-sphere scene (CudaPathTracerKernel.cu semantics) ----------------------------------
+@pytest.mark.parametrize("w,h", [(160, 90), (7, 5), (1, 1), (64, 1)])
+def test_legacy_abi_frames_match_oracle(pt, w, h):
+    assert pt.initialize(w, h), pt.lastError()
+    for _ in range(3):
+        assert pt.renderFrame(8), pt.lastError()
+    assert pt.frameIndex() == 3
+    px = pt.hostPixels()
+    _, acc = pt.readback()
+    ora_px, ora_acc = po.sphere4(w, h, 0, 3, 8)
+    _assert_same(px, acc, ora_px, ora_acc)
+
+
+def test_legacy_reinit_resets_accumulation(pt):
+    # RayTracerFboItem.cpp:520-521 calls initialize again on frame 0
+    assert pt.initialize(32, 16)
+    assert pt.renderFrame(4)
+    assert pt.initialize(32, 16)
+    assert pt.renderFrame(4)
+    ora_px, _ = po.sphere4(32, 16, 0, 1, 4)
+    assert np.array_equal(pt.hostPixels(), ora_px)
+
+
+def test_legacy_batched_frames_equal_single_frames(pt):
+    assert pt.initialize(96, 64)
+    assert pt.renderFrames(5, 6)
+    a = pt.readback()
+    assert pt.initialize(96, 64)
+    for _ in range(5):
+        assert pt.renderFrame(6)
+    b = pt.readback()
+    _assert_same(a[0], a[1], b[0], b[1])
+
+
+@pytest.mark.parametrize("depth", [0, 1, 50])
+def test_legacy_depth_edge_cases(pt, depth):
+    assert pt.initialize(40, 30)
+    assert pt.renderFrames(2, depth)
+    px, acc = pt.readback()
+    ora_px, ora_acc = po.sphere4(40, 30, 0, 2, depth)
+    _assert_same(px, acc, ora_px, ora_acc)
+
+
+# ---- triangle meshes -------------------------------------------------------------------------------
+@pytest.mark.parametrize("name,w,h,spp,depth", [
+    ("cornell34", 96, 64, 8, 8),
+    ("cornell34", 33, 17, 3, 4),
+    ("blob70k", 64, 48, 4, 8),
+    ("blob70k", 17, 9, 2, 2),
+])
+def test_mesh_matches_oracle(pt, name, w, h, spp, depth):
+    sc = scenes.get_scene(name)
+    pt.uploadMesh(sc)
+    assert pt.initialize(w, h), pt.lastError()
+    assert pt.renderFrames(spp, depth), pt.lastError()
+    px, acc = pt.readback()
+    ora_px, ora_acc, segs, samples = po.MeshScene(sc, w, h).frames(0, spp, depth)
+    _assert_same(px, acc, ora_px, ora_acc)
+    st = pt.stats()
+    assert st["segments"] == segs and st["pixelSamples"] == samples
+
+
+def test_mesh_wave_threshold_and_chunk_do_not_change_results(pt):
+    sc = scenes.cornell34()
+    pt.uploadMesh(sc)
+    ref = None
+    for thr, chunk in ((0, 64), (16, 256), (63, 4096), (32, 1024)):
+        pt.setOption(hippt.OPT_WAVE_THRESHOLD, thr)
+        pt.setOption(hippt.OPT_CHUNK, chunk)
+        assert pt.initialize(80, 40)
+        assert pt.renderFrames(4, 8)
+        got = pt.readback()
+        if ref is None:
+            ref = got
+        else:
+            _assert_same(got[0], got[1], ref[0], ref[1])
+
+
+def test_mesh_batches_and_frame_splits_are_bit_identical(pt):
+    sc = scenes.blob70k()
+    pt.uploadMesh(sc)
+    assert pt.initialize(48, 40)
+    assert pt.renderFrames(6, 8)
+    one = pt.readback()
+    pt.setOption(hippt.OPT_SCRATCH_MB, 1)  # forces several scratch batches per call
+    assert pt.initialize(48, 40)
+    for n in (1, 2, 3):
+        assert pt.renderFrames(n, 8)
+    split = pt.readback()
+    _assert_same(one[0], one[1], split[0], split[1])
+
+
+def test_mesh_row_range_and_two_contexts(pt):
+    sc = scenes.cornell34()
+    pt.uploadMesh(sc)
+    w, h = 64, 40
+    assert pt.initialize(w, h)
+    assert pt.renderFrames(3, 8)
+    full = pt.readback()
+    # one process owning rows [13, 29) of the image
+    pt.setRowRange(13, 29)
+    assert pt.initialize(w, h)
+    assert pt.renderFrames(3, 8)
+    band = pt.readback(13, 29)
+    _assert_same(band[0], band[1], full[0][13:29], full[1][13:29])
+    # two contexts (row bands) on the same device: the multi-GPU host gather path
+    pt.setRowRange(0, 0)
+    pt.setDevices([0, 0])
+    assert pt.initialize(w, h)
+    assert pt.renderFrames(3, 8)
+    assert pt.stats()["numDevices"] == 2
+    two = pt.readback()
+    _assert_same(two[0], two[1], full[0], full[1])
+    assert np.array_equal(pt.hostPixels(), full[0])
+
+
+def test_single_triangle_and_degenerate_sizes(pt):
+    v = np.array([[200, 100, 300, 400, 100, 300, 300, 400, 300]], np.float32)
+    sc = scenes.Scene("one", v, np.zeros(1, np.int32), np.array([[0.5, 0.6, 0.7]], np.float32))
+    pt.uploadMesh(sc)
+    for w, h in ((1, 1), (5, 1), (1, 7), (31, 29)):
+        assert pt.initialize(w, h)
+        assert pt.renderFrames(2, 3)
+        px, acc = pt.readback()
+        ora = po.MeshScene(sc, w, h).frames(0, 2, 3)
+        _assert_same(px, acc, ora[0], ora[1])
+
+
+def test_mesh_depth_zero_is_black(pt):
+    pt.uploadMesh(scenes.cornell34())
+    assert pt.initialize(16, 8)
+    assert pt.renderFrames(2, 0)
+    px, acc = pt.readback()
+    assert np.all(px == 0xFF000000) and np.all(acc[..., :3] == 0) and pt.stats()["segments"] == 0
+
+
+def test_full_size_1080p_rows_and_determinism(pt):
+    """BASELINE config 2 size: bit-exact on sampled rows, deterministic, counts consistent."""
+    sc = scenes.cornell34()
+    pt.uploadMesh(sc)
+    w, h, spp = 1920, 1080, 8
+    assert pt.initialize(w, h)
+    assert pt.renderFrames(spp, 8)
+    a = pt.readback()
+    st = pt.stats()
+    assert st["pixelSamples"] == w * h * spp
+    assert st["pixelSamples"] < st["segments"] < 8 * st["pixelSamples"]
+    assert pt.initialize(w, h)
+    assert pt.renderFrames(spp, 8)
+    b = pt.readback()
+    _assert_same(a[0], a[1], b[0], b[1])
+    ms = po.MeshScene(sc, w, h)
+    for y0 in (0, 537, 1078):
+        ora = ms.frames(0, spp, 8, y0=y0, y1=y0 + 2)
+        _assert_same(a[0][y0:y0 + 2], a[1][y0:y0 + 2], ora[0], ora[1])
+
+
+def test_counting_mode_reports_traversal(pt):
+    sc = scenes.blob70k()
+    pt.uploadMesh(sc)
+    pt.setOption(hippt.OPT_COUNT_TRAVERSAL, 1)
+    assert pt.initialize(64, 32)
+    assert pt.renderFrames(2, 8)
+    st = pt.stats()
+    counted = pt.readback()
+    assert st["nodeVisits"] > st["segments"] > 0 and st["triTests"] > 0
+    pt.setOption(hippt.OPT_COUNT_TRAVERSAL, 0)
+    assert pt.initialize(64, 32)
+    assert pt.renderFrames(2, 8)
+    plain = pt.readback()
+    _assert_same(counted[0], counted[1], plain[0], plain[1])
