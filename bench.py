@@ -88,19 +88,22 @@ def cpu_baseline(args, scene) -> dict | None:
             path = os.path.join(tmp, "scene.bin")
             sc_mod.write_scene_file(scene, path)
 
-            def run(rows):
+            def run(stride):
                 out = subprocess.run([pyoracle.REF_HARNESS, "bench", path, str(args.width), str(args.height),
-                                      str(rows), str(args.spp), str(args.depth), str(threads)],
-                                     capture_output=True, text=True, check=True, timeout=600).stdout
+                                      str(stride), str(args.spp), str(args.depth), str(threads)],
+                                     capture_output=True, text=True, check=True, timeout=900).stdout
                 return json.loads(out.strip().splitlines()[-1])
 
-            probe = run(max(1, min(24, args.height)))
-            rows = int(probe["rows"] * args.cpu_seconds / max(probe["seconds"], 1e-3))
-            rows = max(1, min(args.height, rows))
-            r = run(rows)
+            # probe on every 64th line, then pick the line stride that takes ~cpu_seconds
+            probe = run(64)
+            per_line = probe["seconds"] / max(1, probe["rows"])
+            lines = max(1, min(args.height, int(args.cpu_seconds / max(per_line, 1e-6))))
+            stride = max(1, -(-args.height // lines))
+            r = run(stride)
         return {"value": round(r["msamples_per_s"], 4), "unit": "Msamples/s", "cores": threads,
                 "kind": "reference",
-                "sample": f"rows 0..{rows - 1} of {args.width}x{args.height}, {args.spp} spp, depth {args.depth}, "
+                "sample": f"every {stride}th line ({r['rows']} lines) of {args.width}x{args.height}, {args.spp} spp, "
+                          f"depth {args.depth}, "
                           f"{scene.name}; RayTracer.h ray_color + RenderWorker tile pool (tile {r['tile']}), "
                           f"{r['segments']} segments in {r['seconds']:.2f} s",
                 "mpixel_samples_per_s": round(r["mpixel_samples_per_s"], 4)}

@@ -330,8 +330,11 @@ int choose_tile(int w, int h) {
 }
 
 // RenderWorker::render (RayTracerFboItem.cpp:46-144) without Qt; timing only.
-// Renders rows [0, rows) of a W x H image (a bounded sample of the workload).
-int cmd_bench(const char *scene_path, int W, int H, int rows, int spp, int depth, int threads) {
+// Renders every `stride`-th line of a W x H image (a bounded, representative sample of
+// the workload: lines 0, stride, 2*stride, ...), tiled over the compacted lines.
+int cmd_bench(const char *scene_path, int W, int H, int stride, int spp, int depth, int threads) {
+    if (stride < 1) stride = 1;
+    const int rows = (H + stride - 1) / stride;
     Scene s;
     if (!load_scene(scene_path, s)) return 3;
     auto t_setup = std::chrono::steady_clock::now();
@@ -361,7 +364,7 @@ int cmd_bench(const char *scene_path, int W, int H, int rows, int spp, int depth
                 int x0 = (idx % tilesX) * tile, y0 = (idx / tilesX) * tile;
                 int x1 = std::min(x0 + tile, W), y1 = std::min(y0 + tile, rows);
                 for (int line = y0; line < y1; ++line) {
-                    const int j = H - 1 - line;
+                    const int j = H - 1 - line * stride;
                     for (int i = x0; i < x1; ++i) {
                         Color pc(0, 0, 0);
                         for (int k = 0; k < spp; ++k) {
@@ -387,9 +390,9 @@ int cmd_bench(const char *scene_path, int W, int H, int rows, int spp, int depth
     unsigned long long chk = 0;
     for (unsigned p : image) chk = chk * 1315423911ULL + p;
     std::printf("{\"seconds\": %.6f, \"setup_seconds\": %.6f, \"threads\": %d, \"tile\": %d, \"width\": %d, "
-                "\"height\": %d, \"rows\": %d, \"spp\": %d, \"depth\": %d, \"pixel_samples\": %llu, "
+                "\"height\": %d, \"rows\": %d, \"stride\": %d, \"spp\": %d, \"depth\": %d, \"pixel_samples\": %llu, "
                 "\"segments\": %llu, \"msamples_per_s\": %.6f, \"mpixel_samples_per_s\": %.6f, \"checksum\": %llu}\n",
-                secs, setup, threads, tile, W, H, rows, spp, depth, ps, (unsigned long long)segs.load(),
+                secs, setup, threads, tile, W, H, rows, stride, spp, depth, ps, (unsigned long long)segs.load(),
                 double(segs.load()) / secs / 1e6, double(ps) / secs / 1e6, chk);
     return 0;
 }
@@ -408,6 +411,6 @@ int main(int argc, char **argv) {
     std::fprintf(stderr,
                  "usage: ref_harness golden OUT.json [SCENE]\n"
                  "       ref_harness converge SCENE W H SPP DEPTH OUT.f32 [THREADS]\n"
-                 "       ref_harness bench SCENE W H ROWS SPP DEPTH [THREADS]\n");
+                 "       ref_harness bench SCENE W H STRIDE SPP DEPTH [THREADS]\n");
     return 1;
 }

@@ -48,7 +48,8 @@ struct Ctx {
     unsigned long long *stats = nullptr;
     int sceneVersion = -1;
     float4 *nodes = nullptr, *tris = nullptr, *shade = nullptr, *albedo = nullptr;
-    int cus = 0, meshBlocksPerCu[2] = {0, 0};
+    int cus = 0;
+    int occDepth = -1, meshBlocksPerCu[2] = {0, 0};  // occupancy cached per stack depth
     std::vector<EventPair> pool;                         // reusable events
     std::vector<std::pair<int, EventPair>> pending;      // (0 trace / 1 combine, events)
     size_t poolUsed = 0;
@@ -255,8 +256,6 @@ bool init_inner(int width, int height, const char **err) {
         HIP_TRY(hipMemsetAsync(c.out, 0, px * sizeof(uint32_t), c.stream));
         HIP_TRY(hipMemsetAsync(c.stats, 0, 64, c.stream));
         HIP_TRY(hipDeviceGetAttribute(&c.cus, hipDeviceAttributeMultiprocessorCount, c.device));
-        c.meshBlocksPerCu[0] = hippt::mesh_blocks_per_cu(false);
-        c.meshBlocksPerCu[1] = hippt::mesh_blocks_per_cu(true);
         HIP_TRY(hipStreamSynchronize(c.stream));
     }
     s.hostCount = size_t(width) * size_t(height);
@@ -320,6 +319,12 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                     c.scratchBytes = need;
                 }
                 const bool cnt = s.countTraversal;
+                const int stackDepth = std::max(1, s.scene.levels);
+                if (c.occDepth != stackDepth) {
+                    c.meshBlocksPerCu[0] = hippt::mesh_blocks_per_cu(false, stackDepth);
+                    c.meshBlocksPerCu[1] = hippt::mesh_blocks_per_cu(true, stackDepth);
+                    c.occDepth = stackDepth;
+                }
                 int bpc = s.blocksPerCu > 0 ? s.blocksPerCu : c.meshBlocksPerCu[cnt ? 1 : 0];
                 for (int b = 0; b < count; b += fpb) {
                     const int nf = std::min(fpb, count - b);
@@ -348,6 +353,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.maxDepth = maxDepth;
                         p.bandPixels = bandPixels;
                         p.totalItems = total;
+                        p.stackDepth = stackDepth;
                         p.waveThreshold = s.waveThreshold;
                         p.chunk = s.chunk;
                         long long blocks = (long long)c.cus * bpc;

@@ -38,6 +38,7 @@ struct MeshParams {
     int width, height, y0, bandRows;
     int firstFrame, frames, maxDepth;
     unsigned bandPixels, totalItems;
+    int stackDepth;        // LDS stack entries per lane (>= BVH interior levels)
     int waveThreshold;     // shade once fewer than this many lanes still traverse
     unsigned chunk;        // items per queue grab (multiple of 64)
 };
@@ -55,8 +56,8 @@ struct CombineParams {
 hipError_t launch_sphere4(const Sphere4Params &p, hipStream_t s);
 hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hipStream_t s);
 hipError_t launch_combine(const CombineParams &p, hipStream_t s);
-// Resident mesh-kernel blocks per CU (occupancy query).
-int mesh_blocks_per_cu(bool countTraversal);
+// Resident mesh-kernel blocks per CU for a given LDS stack depth (occupancy query).
+int mesh_blocks_per_cu(bool countTraversal, int stackDepth);
 constexpr int kMeshBlock = 256;
 
 }  // namespace hippt

@@ -212,8 +212,11 @@ __device__ __forceinline__ unsigned wave_fetch(bool req, unsigned &poolNext, uns
 
 template <bool STATS>
 __global__ __launch_bounds__(kMeshBlock) void mesh_kernel(MeshParams P) {
-    __shared__ int stk[kStackDepth * kMeshBlock];
-    int *const my = stk + threadIdx.x;  // entry k at my[k * kMeshBlock]: conflict-free per lane
+    // Per-lane traversal stack, P.stackDepth (= BVH interior levels) entries per lane, sized
+    // at launch so shallow BVHs do not cap occupancy.  Entry k of lane t at stk[k*256 + t]:
+    // a wave's lanes hit 64 consecutive dwords, conflict-free for any mix of depths.
+    extern __shared__ int stk[];
+    int *const my = stk + threadIdx.x;
     const float tmin = 0.001f;
 
     unsigned poolNext = 0, poolEnd = 0;
@@ -309,16 +312,19 @@ __global__ __launch_bounds__(kMeshBlock) void mesh_kernel(MeshParams P) {
                 const float n1 = fmaxf(fmaxf(fminf(l1x, h1x), fminf(l1y, h1y)), fmaxf(fminf(l1z, h1z), tmin));
                 const float f1 = fminf(fminf(fmaxf(l1x, h1x), fmaxf(l1y, h1y)), fminf(fmaxf(l1z, h1z), bestT));
                 const bool hit0 = n0 <= f0, hit1 = n1 <= f1;
-                if (hit0 && hit1) {
-                    const bool first0 = n0 <= n1;
-                    my[sp * kMeshBlock] = first0 ? e.y : e.x;  // far child
-                    ++sp;
-                    cur = first0 ? e.x : e.y;
-                } else if (hit0 || hit1) {
-                    cur = hit0 ? e.x : e.y;
-                } else {
-                    cur = sp > 0 ? my[--sp * kMeshBlock] : kDone;
-                }
+                // Branch-free child selection: near child first; the far child is written to
+                // the slot above the top unconditionally (one spare slot per lane), kept only
+                // when both children are hit; the top is read unconditionally and used only
+                // when neither is.
+                const bool take0 = hit0 && (!hit1 || n0 <= n1);
+                const int nearC = take0 ? e.x : e.y;
+                const int farC = take0 ? e.y : e.x;
+                my[sp * kMeshBlock] = farC;
+                const int top = my[max(sp - 1, 0) * kMeshBlock];
+                const bool none = !(hit0 || hit1);
+                sp += (hit0 && hit1) ? 1 : 0;
+                cur = none ? (sp > 0 ? top : kDone) : nearC;
+                sp -= (none && sp > 0) ? 1 : 0;
             }
             while (cur < 0 && cur != kDone) {
                 const int code = ~cur;
@@ -463,11 +469,16 @@ hipError_t launch_sphere4(const Sphere4Params &p, hipStream_t s) {
     return hipGetLastError();
 }
 
+// One spare slot per lane above the deepest level for the speculative far-child write.
+size_t mesh_lds_bytes(int stackDepth) { return size_t(stackDepth + 1) * kMeshBlock * sizeof(int); }
+
 hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hipStream_t s) {
+    if (p.stackDepth < 1 || p.stackDepth > kStackDepth) return hipErrorInvalidValue;
+    const size_t lds = mesh_lds_bytes(p.stackDepth);
     if (countTraversal)
-        hipLaunchKernelGGL(mesh_kernel<true>, dim3(blocks), dim3(kMeshBlock), 0, s, p);
+        hipLaunchKernelGGL(mesh_kernel<true>, dim3(blocks), dim3(kMeshBlock), lds, s, p);
     else
-        hipLaunchKernelGGL(mesh_kernel<false>, dim3(blocks), dim3(kMeshBlock), 0, s, p);
+        hipLaunchKernelGGL(mesh_kernel<false>, dim3(blocks), dim3(kMeshBlock), lds, s, p);
     return hipGetLastError();
 }
 
@@ -479,11 +490,12 @@ hipError_t launch_combine(const CombineParams &p, hipStream_t s) {
     return hipGetLastError();
 }
 
-int mesh_blocks_per_cu(bool countTraversal) {
+int mesh_blocks_per_cu(bool countTraversal, int stackDepth) {
     int n = 0;
+    const size_t lds = mesh_lds_bytes(stackDepth);
     hipError_t e = countTraversal
-                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mesh_kernel<true>, kMeshBlock, 0)
-                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mesh_kernel<false>, kMeshBlock, 0);
+                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mesh_kernel<true>, kMeshBlock, lds)
+                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mesh_kernel<false>, kMeshBlock, lds);
     if (e != hipSuccess || n <= 0) n = 1;
     return n;
 }
