@@ -120,6 +120,12 @@ typedef struct hipptStats {
 
 bool hipptGetStats(hipptStats *out);
 void hipptResetStats(void);
+/* Raw device counters (profiling): [0] segments, [1] pixel samples, [2] node visits,
+ * [3] triangle tests, [4 + 2k] / [5 + 2k] wave-level / lane-level passes of mesh-kernel
+ * phase k (HIPPT_OPT_COUNT_TRAVERSAL builds only): 0 outer loop, 1 camera ray, 2 traversal
+ * round, 3 interior node, 4 leaf, 5 triangle, 6 shading, 7 unit-sphere rejection.
+ * Returns the number of words written (<= n, <= 32). */
+int hipptGetCounters(unsigned long long *out, int n);
 
 enum {
     HIPPT_OPT_COUNT_TRAVERSAL = 1,  /* 1: count node visits / triangle tests (slower) */

@@ -32,6 +32,8 @@ namespace {
 
 using hippt::CameraF;
 
+constexpr int kStatWords = 32;  // [0..3] hipptStats counters, [4..19] phase profile
+
 struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
 };
@@ -79,7 +81,7 @@ struct State {
     char error[256] = {0};
     // options
     bool countTraversal = false;
-    int waveThreshold = 16;
+    int waveThreshold = 32;
     long long scratchMB = 256;
     unsigned chunk = 256;
     int blocksPerCu = 0;
@@ -251,10 +253,10 @@ bool init_inner(int width, int height, const char **err) {
         HIP_TRY(hipMalloc(&c.accum, std::max<size_t>(16, px * sizeof(float4))));
         HIP_TRY(hipMalloc(&c.out, std::max<size_t>(16, px * sizeof(uint32_t))));
         HIP_TRY(hipMalloc(&c.queue, 64));
-        HIP_TRY(hipMalloc(&c.stats, 64));
+        HIP_TRY(hipMalloc(&c.stats, kStatWords * sizeof(unsigned long long)));
         HIP_TRY(hipMemsetAsync(c.accum, 0, px * sizeof(float4), c.stream));
         HIP_TRY(hipMemsetAsync(c.out, 0, px * sizeof(uint32_t), c.stream));
-        HIP_TRY(hipMemsetAsync(c.stats, 0, 64, c.stream));
+        HIP_TRY(hipMemsetAsync(c.stats, 0, kStatWords * sizeof(unsigned long long), c.stream));
         HIP_TRY(hipDeviceGetAttribute(&c.cus, hipDeviceAttributeMultiprocessorCount, c.device));
         HIP_TRY(hipStreamSynchronize(c.stream));
     }
@@ -630,6 +632,23 @@ extern "C" bool hipptGetStats(hipptStats *out) {
     return true;
 }
 
+extern "C" int hipptGetCounters(unsigned long long *out, int n) {
+    std::lock_guard<std::mutex> g(S().mu);
+    State &s = S();
+    if (!out || n <= 0) return 0;
+    n = std::min(n, kStatWords);
+    std::memset(out, 0, sizeof(unsigned long long) * size_t(n));
+    const char *err = nullptr;
+    if (s.ready && !sync_locked(&err)) return 0;
+    for (Ctx &c : s.ctxs) {
+        unsigned long long v[kStatWords];
+        if (hipSetDevice(c.device) != hipSuccess) return 0;
+        if (hipMemcpy(v, c.stats, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return 0;
+        for (int i = 0; i < n; ++i) out[i] += v[i];
+    }
+    return n;
+}
+
 extern "C" void hipptResetStats(void) {
     std::lock_guard<std::mutex> g(S().mu);
     State &s = S();
@@ -637,7 +656,7 @@ extern "C" void hipptResetStats(void) {
     if (s.ready) sync_locked(&err);
     for (Ctx &c : s.ctxs) {
         (void)hipSetDevice(c.device);
-        (void)hipMemset(c.stats, 0, 64);
+        (void)hipMemset(c.stats, 0, kStatWords * sizeof(unsigned long long));
     }
     s.traceMs = s.combineMs = 0;
     s.traceLaunches = s.combineLaunches = 0;

@@ -210,6 +210,18 @@ __device__ __forceinline__ unsigned wave_fetch(bool req, unsigned &poolNext, uns
     return (req && item < total) ? item : kNone;
 }
 
+// Phase profiling (STATS build only): pc[2k] counts wave-level passes of phase k (by the
+// first active lane), pc[2k+1] lane-level passes; SIMD efficiency = lanes / (64 * waves).
+// Phases: 0 outer iteration, 1 camera-ray generation, 2 traversal do-while, 3 interior node
+// loop, 4 leaf loop, 5 triangle loop, 6 shading, 7 unit-sphere rejection loop.
+#define HIPPT_PROF(k)                                                                     \
+    do {                                                                                  \
+        if (STATS) {                                                                      \
+            ++pc[2 * (k) + 1];                                                            \
+            if (__lane_id() == unsigned(__ffsll((unsigned long long)__ballot(1)) - 1)) ++pc[2 * (k)]; \
+        }                                                                                 \
+    } while (0)
+
 template <bool STATS>
 __global__ __launch_bounds__(kMeshBlock) void mesh_kernel(MeshParams P) {
     // Per-lane traversal stack, P.stackDepth (= BVH interior levels) entries per lane, sized
@@ -228,10 +240,12 @@ __global__ __launch_bounds__(kMeshBlock) void mesh_kernel(MeshParams P) {
     float ix = 0, iy = 0, iz = 0, oix = 0, oiy = 0, oiz = 0;
     float tr = 1, tg = 1, tb = 1;
     int cur = kDone, sp = 0;
+    int leaf = 0;  // postponed leaf code (< 0) or 0 = none
     float bestT = INFINITY;
     int bestI = -1, bestO = 0x7fffffff;
     bool need = true;
     unsigned long long segs = 0, samples = 0, nvis = 0, ntest = 0;
+    unsigned pc[16] = {0};
 
     auto begin_traversal = [&]() {
         // Fast reciprocal; |d| clamped so that o*inv stays finite (box test only).
@@ -252,6 +266,7 @@ __global__ __launch_bounds__(kMeshBlock) void mesh_kernel(MeshParams P) {
     };
 
     for (;;) {
+        HIPPT_PROF(0);
         // ---- refill: every lane whose sample ended takes the next (pixel, frame) -------------
         if (__ballot(need)) {
             const unsigned it = wave_fetch(need, poolNext, poolEnd, P.queue, P.chunk, P.totalItems);
@@ -259,6 +274,7 @@ __global__ __launch_bounds__(kMeshBlock) void mesh_kernel(MeshParams P) {
                 need = false;
                 item = it;
                 if (it != kNone) {
+                    HIPPT_PROF(1);
                     // RenderWorker::render u/v (RayTracerFboItem.cpp:109-110), Camera::get_ray
                     // (RayTracer.h:563-567), seed per CudaPathTracerKernel.cu:144.
                     const unsigned fl = it / P.bandPixels;
@@ -296,7 +312,9 @@ __global__ __launch_bounds__(kMeshBlock) void mesh_kernel(MeshParams P) {
 
         // ---- traversal: while-while over the BVH; leave once few lanes remain -------------
         do {
+            HIPPT_PROF(2);
             while (cur >= 0) {
+                HIPPT_PROF(3);
                 const float4 *nd = P.nodes + 4 * cur;
                 const float4 a = nd[0], b = nd[1], c = nd[2];
                 const int4 e = *reinterpret_cast<const int4 *>(nd + 3);
@@ -325,13 +343,23 @@ __global__ __launch_bounds__(kMeshBlock) void mesh_kernel(MeshParams P) {
                 sp += (hit0 && hit1) ? 1 : 0;
                 cur = none ? (sp > 0 ? top : kDone) : nearC;
                 sp -= (none && sp > 0) ? 1 : 0;
+                // Speculative traversal (Aila & Laine 2009): postpone the first leaf reached and
+                // keep descending, so the wave enters the leaf loop only once every lane still
+                // in this loop holds a leaf.
+                if (cur < 0 && cur != kDone && leaf == 0) {
+                    leaf = cur;
+                    cur = sp > 0 ? my[--sp * kMeshBlock] : kDone;
+                }
+                if (!__any(leaf == 0)) break;
             }
-            while (cur < 0 && cur != kDone) {
-                const int code = ~cur;
+            while (leaf != 0) {
+                HIPPT_PROF(4);
+                const int code = ~leaf;
                 const int first = code >> 4, last = first + (code & 15);
                 for (int i = first; i < last; ++i) {
                     const float4 *tp = P.tris + 3 * i;
                     const float4 A = tp[0], B = tp[1], Cc = tp[2];
+                    HIPPT_PROF(5);
                     if (STATS) ++ntest;
                     // Möller–Trumbore, division-free edge tests (pt_oracle.c po_tri_hit)
                     const float e1x = A.w, e1y = B.x, e1z = B.y;
@@ -358,12 +386,18 @@ __global__ __launch_bounds__(kMeshBlock) void mesh_kernel(MeshParams P) {
                         }
                     }
                 }
-                cur = sp > 0 ? my[--sp * kMeshBlock] : kDone;
+                // a leaf that was next in line is processed in the same loop
+                leaf = 0;
+                if (cur < 0 && cur != kDone) {
+                    leaf = cur;
+                    cur = sp > 0 ? my[--sp * kMeshBlock] : kDone;
+                }
             }
         } while (__popcll(__ballot(cur != kDone)) > unsigned(P.waveThreshold));
 
         // ---- shading: lanes whose traversal finished (ray_color step, RayTracer.h:579-596) ----
         if (item != kNone && cur == kDone) {
+            HIPPT_PROF(6);
             ++segs;
             bool finished = false;
             float Lr = 0.0f, Lg = 0.0f, Lb = 0.0f;
@@ -388,6 +422,7 @@ __global__ __launch_bounds__(kMeshBlock) void mesh_kernel(MeshParams P) {
                 }
                 float rx, ry, rz, r2;
                 for (;;) {  // random_in_unit_sphere, :155-161
+                    HIPPT_PROF(7);
                     rx = fmaf(2.0f, rand01(rng), -1.0f);
                     ry = fmaf(2.0f, rand01(rng), -1.0f);
                     rz = fmaf(2.0f, rand01(rng), -1.0f);
@@ -438,7 +473,15 @@ __global__ __launch_bounds__(kMeshBlock) void mesh_kernel(MeshParams P) {
             atomicAdd(&P.stats[3], ntest);
         }
     }
+    if (STATS) {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+            const unsigned long long v = wave_sum(pc[k]);
+            if (__lane_id() == 0) atomicAdd(&P.stats[4 + k], v);
+        }
+    }
 }
+#undef HIPPT_PROF
 
 // Running average in frame order, then ARGB (CudaPathTracerKernel.cu:157-178).
 __global__ __launch_bounds__(256) void combine_kernel(CombineParams P) {

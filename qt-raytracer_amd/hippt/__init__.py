@@ -39,7 +39,8 @@ EXPORTS = (
     "hipptBuildCamera", "hipptUseBuiltinScene", "hipptUploadMesh", "hipptSetCamera",
     "hipptDeviceCount", "hipptSetDevices", "hipptSetRowRange",
     "hipptRenderFrames", "hipptRenderFramesAsync", "hipptSynchronize", "hipptReadback",
-    "hipptResetAccumulation", "hipptGetStats", "hipptResetStats", "hipptSetOption", "hipptGetOption",
+    "hipptResetAccumulation", "hipptGetStats", "hipptResetStats", "hipptGetCounters", "hipptSetOption",
+    "hipptGetOption",
     "hipptLastError", "hipptBvhBuild", "hipptBvhNodeCount", "hipptBvhDepth", "hipptBvhCopy", "hipptBvhFree",
 )
 
@@ -115,6 +116,7 @@ def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
     sig("hipptResetAccumulation", c_bool, pp_char)
     sig("hipptGetStats", c_bool, ctypes.POINTER(Stats))
     sig("hipptResetStats", None)
+    sig("hipptGetCounters", c_int, ctypes.POINTER(ctypes.c_ulonglong), c_int)
     sig("hipptSetOption", c_bool, c_int, ctypes.c_longlong)
     sig("hipptGetOption", ctypes.c_longlong, c_int)
     sig("hipptLastError", c_char_p)
@@ -305,6 +307,19 @@ class PathTracer:
         if not self._lib.hipptGetStats(ctypes.byref(s)):
             raise HipptError("hipptGetStats failed")
         return s.as_dict()
+
+    PHASES = ("outer", "camera", "traversal_round", "node", "leaf", "triangle", "shade", "sphere_reject")
+
+    def counters(self) -> dict:
+        """Raw device counters incl. per-phase SIMD efficiency (counting builds)."""
+        buf = (ctypes.c_ulonglong * 32)()
+        n = self._lib.hipptGetCounters(buf, 32)
+        v = list(buf)[:n]
+        out = {"segments": v[0], "pixelSamples": v[1], "nodeVisits": v[2], "triTests": v[3]}
+        for k, name in enumerate(self.PHASES):
+            w, l = v[4 + 2 * k], v[5 + 2 * k]
+            out[name] = {"wave": w, "lane": l, "simd_eff": round(l / (64 * w), 4) if w else None}
+        return out
 
     def resetStats(self) -> None:  # noqa: N802
         self._lib.hipptResetStats()

@@ -20,7 +20,7 @@ def pt():
     t.setDevices([])
     t.setRowRange(0, 0)
     t.useBuiltinScene(hippt.SCENE_SPHERE4)
-    for k, v in ((hippt.OPT_WAVE_THRESHOLD, 16), (hippt.OPT_SCRATCH_MB, 256), (hippt.OPT_CHUNK, 256),
+    for k, v in ((hippt.OPT_WAVE_THRESHOLD, 32), (hippt.OPT_SCRATCH_MB, 256), (hippt.OPT_CHUNK, 256),
                  (hippt.OPT_COUNT_TRAVERSAL, 0), (hippt.OPT_BLOCKS_PER_CU, 0)):
         t.setOption(k, v)
     t.resetStats()

@@ -1,0 +1,65 @@
+#!/usr/bin/env python3
+"""Option sweep in one process (GPU box): Msamples/s per libhippt option setting.
+
+usage: python tools/sweep.py [--scene cornell34] [--steps 3] KEY=v1,v2 [KEY=...]
+keys: wave (HIPPT_OPT_WAVE_THRESHOLD), chunk, scratch (MB), bpc (blocks per CU)
+Each combination: one warmup step, then `steps` timed steps; prints one JSON line each.
+"""
+from __future__ import annotations
+
+import argparse
+import itertools
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "qt-raytracer_amd"))
+
+import hippt  # noqa: E402
+from hippt import scenes  # noqa: E402
+
+KEYS = {"wave": hippt.OPT_WAVE_THRESHOLD, "chunk": hippt.OPT_CHUNK, "scratch": hippt.OPT_SCRATCH_MB,
+        "bpc": hippt.OPT_BLOCKS_PER_CU}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--scene", default="cornell34")
+    ap.add_argument("--width", type=int, default=1920)
+    ap.add_argument("--height", type=int, default=1080)
+    ap.add_argument("--spp", type=int, default=64)
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("grid", nargs="*")
+    a = ap.parse_args()
+    axes = []
+    for g in a.grid:
+        k, vs = g.split("=")
+        axes.append([(k, int(v)) for v in vs.split(",")])
+    pt = hippt.PathTracer()
+    pt.setDevices([0])
+    sc = scenes.get_scene(a.scene)
+    pt.uploadMesh(sc)
+    for combo in itertools.product(*axes) if axes else [()]:
+        for k, v in combo:
+            pt.setOption(KEYS[k], v)
+        if not pt.initialize(a.width, a.height):
+            raise SystemExit(pt.lastError())
+        pt.renderFrames(a.spp, a.depth, copy=False)
+        pt.resetStats()
+        t0 = time.perf_counter()
+        for _ in range(a.steps):
+            pt._lib.hipptRenderFramesAsync(0, a.spp, a.depth, None)
+        pt.synchronize()
+        dt = time.perf_counter() - t0
+        st = pt.stats()
+        print(json.dumps({"scene": a.scene, **dict(combo), "msamples_s": round(st["segments"] / dt / 1e6, 1),
+                          "trace_ms_step": round(st["traceMs"] / a.steps, 3),
+                          "combine_ms_step": round(st["combineMs"] / a.steps, 3),
+                          "launches_step": st["traceLaunches"] // a.steps}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
