@@ -39,6 +39,8 @@ sys.path.insert(0, os.path.join(REPO, "qt-raytracer_amd"))
 METRIC = "Msamples/s (rays×bounces/s) at 1920×1080, 8 bounces; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0
 BYTES_NODE, BYTES_TRI, BYTES_SHADE, BYTES_SAMPLE = 64, 48, 32, 12
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector (= FP32 MFMA) peak
+FLOP_NODE, FLOP_TRI, FLOP_SHADE = 40, 55, 100  # SURVEY.md §8(d) secondary figure
 
 
 def log(*a):
@@ -220,6 +222,8 @@ def main():
                       + BYTES_SHADE * (counted["segments"] - counted["pixelSamples"])
                       + BYTES_SAMPLE * counted["pixelSamples"])
     alg_bytes_launch = alg_bytes_step / launches
+    flops_launch = (FLOP_NODE * counted["nodeVisits"] + FLOP_TRI * counted["triTests"]
+                    + FLOP_SHADE * counted["segments"]) / launches
     mean_launch_ms = st["traceMs"] / max(1, st["traceLaunches"])
     achieved = alg_bytes_launch / (mean_launch_ms * 1e-3) / 1e9 if mean_launch_ms > 0 else 0.0
     workload = f"{args.scene} {args.width}x{args.height} {args.spp}spp depth{args.depth}"
@@ -263,6 +267,11 @@ def main():
                 "launches_per_step": launches,
                 "alg_bytes_per_launch": int(alg_bytes_launch),
                 "node_visits_per_step": counted["nodeVisits"], "tri_tests_per_step": counted["triTests"],
+                "valu": {"achieved": round(flops_launch / (mean_launch_ms * 1e-3) / 1e12, 3) if mean_launch_ms else 0.0,
+                         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(flops_launch / (mean_launch_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4)
+                         if mean_launch_ms else 0.0,
+                         "model": "40 FLOP/node visit (2 slab tests), 55/triangle test, 100/shading step"},
             },
             "cpu_baseline": cpu,
         }

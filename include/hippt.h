@@ -132,7 +132,8 @@ enum {
     HIPPT_OPT_WAVE_THRESHOLD = 2,   /* lanes still traversing below which a wave goes to shade */
     HIPPT_OPT_SCRATCH_MB = 3,       /* cap of the per-batch sample scratch per device */
     HIPPT_OPT_CHUNK = 4,            /* work items a wave takes from the global queue at once */
-    HIPPT_OPT_BLOCKS_PER_CU = 5     /* persistent-grid residency (0 = occupancy query) */
+    HIPPT_OPT_BLOCKS_PER_CU = 5,    /* persistent-grid residency (0 = occupancy query) */
+    HIPPT_OPT_LDS_SCENE = 6         /* 1 (default): small scenes are copied into LDS per block */
 };
 bool hipptSetOption(int key, long long value);
 long long hipptGetOption(int key);

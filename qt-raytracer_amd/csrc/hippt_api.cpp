@@ -85,6 +85,7 @@ struct State {
     long long scratchMB = 256;
     unsigned chunk = 256;
     int blocksPerCu = 0;
+    bool ldsScene = true;
     // host-side timing accumulators
     double traceMs = 0, combineMs = 0;
     int traceLaunches = 0, combineLaunches = 0;
@@ -322,10 +323,16 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 }
                 const bool cnt = s.countTraversal;
                 const int stackDepth = std::max(1, s.scene.levels);
-                if (c.occDepth != stackDepth) {
-                    c.meshBlocksPerCu[0] = hippt::mesh_blocks_per_cu(false, stackDepth);
-                    c.meshBlocksPerCu[1] = hippt::mesh_blocks_per_cu(true, stackDepth);
-                    c.occDepth = stackDepth;
+                const int numNodes = s.scene.numNodes, numTris = s.scene.numTris;
+                // small scenes live in LDS (scene bytes beyond the stack under the limit)
+                const bool ldsScene =
+                    s.ldsScene && hippt::mesh_lds_bytes(0, numNodes, numTris) <= hippt::mesh_lds_scene_limit();
+                const int occKey = stackDepth * 2 + (ldsScene ? 1 : 0);
+                if (c.occDepth != occKey) {
+                    const int ln = ldsScene ? numNodes : 0, lt = ldsScene ? numTris : 0;
+                    c.meshBlocksPerCu[0] = hippt::mesh_blocks_per_cu(false, stackDepth, ln, lt);
+                    c.meshBlocksPerCu[1] = hippt::mesh_blocks_per_cu(true, stackDepth, ln, lt);
+                    c.occDepth = occKey;
                 }
                 int bpc = s.blocksPerCu > 0 ? s.blocksPerCu : c.meshBlocksPerCu[cnt ? 1 : 0];
                 for (int b = 0; b < count; b += fpb) {
@@ -355,7 +362,12 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.maxDepth = maxDepth;
                         p.bandPixels = bandPixels;
                         p.totalItems = total;
+                        p.rcpBandPixels = 1.0f / float(bandPixels);
+                        p.rcpWidth = 1.0f / float(s.width);
                         p.stackDepth = stackDepth;
+                        p.numNodes = numNodes;
+                        p.numTris = numTris;
+                        p.ldsScene = ldsScene ? 1 : 0;
                         p.waveThreshold = s.waveThreshold;
                         p.chunk = s.chunk;
                         long long blocks = (long long)c.cus * bpc;
@@ -683,6 +695,7 @@ extern "C" bool hipptSetOption(int key, long long value) {
         if (value < 0 || value > 8) return false;
         s.blocksPerCu = int(value);
         return true;
+    case HIPPT_OPT_LDS_SCENE: s.ldsScene = value != 0; return true;
     default: return false;
     }
 }
@@ -696,6 +709,7 @@ extern "C" long long hipptGetOption(int key) {
     case HIPPT_OPT_SCRATCH_MB: return s.scratchMB;
     case HIPPT_OPT_CHUNK: return s.chunk;
     case HIPPT_OPT_BLOCKS_PER_CU: return s.blocksPerCu;
+    case HIPPT_OPT_LDS_SCENE: return s.ldsScene ? 1 : 0;
     default: return -1;
     }
 }

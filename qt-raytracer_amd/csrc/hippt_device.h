@@ -38,7 +38,10 @@ struct MeshParams {
     int width, height, y0, bandRows;
     int firstFrame, frames, maxDepth;
     unsigned bandPixels, totalItems;
+    float rcpBandPixels, rcpWidth;  // 1/bandPixels, 1/width for the item -> (frame, x, y) split
     int stackDepth;        // LDS stack entries per lane (>= BVH interior levels)
+    int numNodes, numTris;
+    int ldsScene;          // 1: copy nodes/triangles/shading into LDS (small scenes)
     int waveThreshold;     // shade once fewer than this many lanes still traverse
     unsigned chunk;        // items per queue grab (multiple of 64)
 };
@@ -56,8 +59,10 @@ struct CombineParams {
 hipError_t launch_sphere4(const Sphere4Params &p, hipStream_t s);
 hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hipStream_t s);
 hipError_t launch_combine(const CombineParams &p, hipStream_t s);
-// Resident mesh-kernel blocks per CU for a given LDS stack depth (occupancy query).
-int mesh_blocks_per_cu(bool countTraversal, int stackDepth);
+// Resident mesh-kernel blocks per CU for a given LDS stack depth and LDS scene size.
+int mesh_blocks_per_cu(bool countTraversal, int stackDepth, int ldsNodes, int ldsTris);
+size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris);
+size_t mesh_lds_scene_limit();
 constexpr int kMeshBlock = 256;
 
 }  // namespace hippt

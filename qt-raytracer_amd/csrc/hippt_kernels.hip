@@ -57,6 +57,22 @@ __device__ __forceinline__ float fdot(float ax, float ay, float az, float bx, fl
     return fmaf(ax, bx, fmaf(ay, by, az * bz));
 }
 
+// n = q*d + r for n < 2^31, d >= 1: float estimate (relative error < 2^-22, so off by at
+// most one for quotients < 2^20) and one exact integer correction — a few VALU instead of
+// the ~30-instruction generic unsigned division.
+__device__ __forceinline__ void divmod(unsigned n, unsigned d, float rcp, unsigned &q, unsigned &r) {
+    q = unsigned(float(n) * rcp);
+    int rem = int(n - q * d);
+    if (rem < 0) {
+        --q;
+        rem += int(d);
+    } else if (rem >= int(d)) {
+        ++q;
+        rem -= int(d);
+    }
+    r = unsigned(rem);
+}
+
 __device__ __forceinline__ unsigned q8(float c) {
     return unsigned(sqrtf(fminf(fmaxf(c, 0.0f), 1.0f)) * 255.0f);
 }
@@ -222,14 +238,40 @@ __device__ __forceinline__ unsigned wave_fetch(bool req, unsigned &poolNext, uns
         }                                                                                 \
     } while (0)
 
-template <bool STATS>
-__global__ __launch_bounds__(kMeshBlock) void mesh_kernel(MeshParams P) {
+// Build knob (experiments): minimum waves per SIMD the register allocator must allow.
+#ifndef HIPPT_MESH_WAVES_PER_EU
+#define HIPPT_MESH_WAVES_PER_EU 1
+#endif
+
+// LDS-resident scene (small scenes): nodes at an 80-byte stride (20 dwords: 16 nodes start on
+// 16 distinct 4-bank groups, so ds_read_b128 of different nodes in a lane group do not
+// conflict), triangles at 48 bytes (12 dwords, likewise), shading records at 16 bytes.
+constexpr int kLdsNodeF4 = 5;
+
+template <bool STATS, bool LDS_SCENE>
+__global__ __launch_bounds__(kMeshBlock, HIPPT_MESH_WAVES_PER_EU) void mesh_kernel(MeshParams P) {
     // Per-lane traversal stack, P.stackDepth (= BVH interior levels) entries per lane, sized
     // at launch so shallow BVHs do not cap occupancy.  Entry k of lane t at stk[k*256 + t]:
     // a wave's lanes hit 64 consecutive dwords, conflict-free for any mix of depths.
     extern __shared__ int stk[];
     int *const my = stk + threadIdx.x;
     const float tmin = 0.001f;
+
+    const float4 *nodes = P.nodes, *tris = P.tris, *shade = P.shade;
+    if (LDS_SCENE) {
+        float4 *sNodes = reinterpret_cast<float4 *>(stk + (P.stackDepth + 1) * kMeshBlock);
+        float4 *sTris = sNodes + P.numNodes * kLdsNodeF4;
+        float4 *sShade = sTris + P.numTris * 3;
+        for (int i = threadIdx.x; i < P.numNodes * 4; i += kMeshBlock)
+            sNodes[(i >> 2) * kLdsNodeF4 + (i & 3)] = P.nodes[i];
+        for (int i = threadIdx.x; i < P.numTris * 3; i += kMeshBlock) sTris[i] = P.tris[i];
+        for (int i = threadIdx.x; i < P.numTris; i += kMeshBlock) sShade[i] = P.shade[i];
+        __syncthreads();
+        nodes = sNodes;
+        tris = sTris;
+        shade = sShade;
+    }
+    constexpr int nodeF4 = LDS_SCENE ? kLdsNodeF4 : 4;
 
     unsigned poolNext = 0, poolEnd = 0;
 
@@ -277,10 +319,9 @@ __global__ __launch_bounds__(kMeshBlock) void mesh_kernel(MeshParams P) {
                     HIPPT_PROF(1);
                     // RenderWorker::render u/v (RayTracerFboItem.cpp:109-110), Camera::get_ray
                     // (RayTracer.h:563-567), seed per CudaPathTracerKernel.cu:144.
-                    const unsigned fl = it / P.bandPixels;
-                    const unsigned p = it - fl * P.bandPixels;
-                    const unsigned yb = p / unsigned(P.width);
-                    const unsigned x = p - yb * unsigned(P.width);
+                    unsigned fl, p, yb, x;
+                    divmod(it, P.bandPixels, P.rcpBandPixels, fl, p);
+                    divmod(p, unsigned(P.width), P.rcpWidth, yb, x);
                     const unsigned y = unsigned(P.y0) + yb;
                     rng = pixel_seed(x, y, unsigned(P.width), unsigned(P.firstFrame) + fl);
                     const float s = (float(x) + rand01(rng)) * P.invW;
@@ -315,7 +356,7 @@ __global__ __launch_bounds__(kMeshBlock) void mesh_kernel(MeshParams P) {
             HIPPT_PROF(2);
             while (cur >= 0) {
                 HIPPT_PROF(3);
-                const float4 *nd = P.nodes + 4 * cur;
+                const float4 *nd = nodes + nodeF4 * cur;
                 const float4 a = nd[0], b = nd[1], c = nd[2];
                 const int4 e = *reinterpret_cast<const int4 *>(nd + 3);
                 if (STATS) ++nvis;
@@ -334,7 +375,7 @@ __global__ __launch_bounds__(kMeshBlock) void mesh_kernel(MeshParams P) {
                 // the slot above the top unconditionally (one spare slot per lane), kept only
                 // when both children are hit; the top is read unconditionally and used only
                 // when neither is.
-                const bool take0 = hit0 && (!hit1 || n0 <= n1);
+                const bool take0 = hit0 & (!hit1 | (n0 <= n1));  // bitwise: no exec-mask branches
                 const int nearC = take0 ? e.x : e.y;
                 const int farC = take0 ? e.y : e.x;
                 my[sp * kMeshBlock] = farC;
@@ -357,7 +398,7 @@ __global__ __launch_bounds__(kMeshBlock) void mesh_kernel(MeshParams P) {
                 const int code = ~leaf;
                 const int first = code >> 4, last = first + (code & 15);
                 for (int i = first; i < last; ++i) {
-                    const float4 *tp = P.tris + 3 * i;
+                    const float4 *tp = tris + 3 * i;
                     const float4 A = tp[0], B = tp[1], Cc = tp[2];
                     HIPPT_PROF(5);
                     if (STATS) ++ntest;
@@ -412,7 +453,7 @@ __global__ __launch_bounds__(kMeshBlock) void mesh_kernel(MeshParams P) {
             } else if (++depth >= P.maxDepth) {
                 finished = true;  // depth exhausted: contributes 0 (RayTracer.h:582-583)
             } else {
-                const float4 sh = P.shade[bestI];
+                const float4 sh = shade[bestI];
                 float nx = sh.x, ny = sh.y, nz = sh.z;
                 const float px = fmaf(bestT, dx, ox), py = fmaf(bestT, dy, oy), pz = fmaf(bestT, dz, oz);
                 if (!(fdot(dx, dy, dz, nx, ny, nz) < 0.0f)) {  // set_face_normal, :215-218
@@ -512,16 +553,26 @@ hipError_t launch_sphere4(const Sphere4Params &p, hipStream_t s) {
     return hipGetLastError();
 }
 
-// One spare slot per lane above the deepest level for the speculative far-child write.
-size_t mesh_lds_bytes(int stackDepth) { return size_t(stackDepth + 1) * kMeshBlock * sizeof(int); }
+// Stack: one spare slot per lane above the deepest level for the speculative far-child
+// write; then (LDS_SCENE) the scene copy.
+size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris) {
+    return size_t(stackDepth + 1) * kMeshBlock * sizeof(int) + size_t(ldsNodes) * kLdsNodeF4 * 16 +
+           size_t(ldsTris) * (3 + 1) * 16;
+}
+
+size_t mesh_lds_scene_limit() { return 24u << 10; }
+
+using MeshFn = void (*)(MeshParams);
+static MeshFn mesh_fn(bool count, bool lds) {
+    if (count) return lds ? mesh_kernel<true, true> : mesh_kernel<true, false>;
+    return lds ? mesh_kernel<false, true> : mesh_kernel<false, false>;
+}
 
 hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hipStream_t s) {
     if (p.stackDepth < 1 || p.stackDepth > kStackDepth) return hipErrorInvalidValue;
-    const size_t lds = mesh_lds_bytes(p.stackDepth);
-    if (countTraversal)
-        hipLaunchKernelGGL(mesh_kernel<true>, dim3(blocks), dim3(kMeshBlock), lds, s, p);
-    else
-        hipLaunchKernelGGL(mesh_kernel<false>, dim3(blocks), dim3(kMeshBlock), lds, s, p);
+    const bool lds = p.ldsScene != 0;
+    const size_t bytes = mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0);
+    hipLaunchKernelGGL(mesh_fn(countTraversal, lds), dim3(blocks), dim3(kMeshBlock), bytes, s, p);
     return hipGetLastError();
 }
 
@@ -533,12 +584,11 @@ hipError_t launch_combine(const CombineParams &p, hipStream_t s) {
     return hipGetLastError();
 }
 
-int mesh_blocks_per_cu(bool countTraversal, int stackDepth) {
+int mesh_blocks_per_cu(bool countTraversal, int stackDepth, int ldsNodes, int ldsTris) {
     int n = 0;
-    const size_t lds = mesh_lds_bytes(stackDepth);
-    hipError_t e = countTraversal
-                       ? hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mesh_kernel<true>, kMeshBlock, lds)
-                       : hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mesh_kernel<false>, kMeshBlock, lds);
+    const bool lds = ldsNodes > 0;
+    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mesh_fn(countTraversal, lds), kMeshBlock, bytes);
     if (e != hipSuccess || n <= 0) n = 1;
     return n;
 }

@@ -31,6 +31,7 @@ OPT_WAVE_THRESHOLD = 2
 OPT_SCRATCH_MB = 3
 OPT_CHUNK = 4
 OPT_BLOCKS_PER_CU = 5
+OPT_LDS_SCENE = 6
 
 # Every symbol include/hippt.h declares (checked by tests/test_abi_cpu.py).
 EXPORTS = (
@@ -74,11 +75,13 @@ class Stats(ctypes.Structure):
 _lib: Optional[ctypes.CDLL] = None
 
 
-def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Loads libhippt.so and declares the C signatures.  Raises if it is missing."""
+def load_library(path: Optional[str] = None) -> ctypes.CDLL:
+    """Loads libhippt.so (or $HIPPT_LIB, for build-variant experiments) and declares the C
+    signatures.  Raises if it is missing."""
     global _lib
     if _lib is not None:
         return _lib
+    path = path or os.environ.get("HIPPT_LIB") or LIB_PATH
     if not os.path.exists(path):
         raise HipptError(f"{path} is missing: build it with `make -C qt-raytracer_amd` "
                          "(or __graft_entry__.build()); there is no fallback path")

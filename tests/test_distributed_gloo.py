@@ -1,0 +1,74 @@
+"""Multi-process row banding on CPU (gloo, world_size 2): the host logic bench.py uses for
+N GPUs — band split, max/sum over ranks, and the host gather of ARGB bands — with the CPU
+oracle standing in for each rank's GPU render (test infrastructure only)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from hippt import distributed as hd
+from hippt import scenes
+
+W, H, SPP, DEPTH = 40, 27, 2, 4
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, out_dir):
+    import pyoracle as po
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        y0, y1 = hd.row_band(rank, world, H)
+        ms = po.MeshScene(scenes.cornell34(), W, H)
+        px, acc, segs, samples = ms.frames(0, SPP, DEPTH, y0=y0, y1=y1, nthreads=1)
+        full_px = hd.gather_bands(px, H, dist)
+        full_acc = hd.gather_bands(acc, H, dist)
+        total_segs = hd.sum_over_ranks(segs, dist)
+        slowest = hd.max_over_ranks(float(rank + 1), dist)
+        if rank == 0:
+            np.save(os.path.join(out_dir, "px.npy"), full_px)
+            np.save(os.path.join(out_dir, "acc.npy"), full_acc)
+            np.save(os.path.join(out_dir, "meta.npy"), np.array([total_segs, slowest], np.float64))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_row_bands_gather_to_single_process_image(tmp_path, world):
+    import pyoracle as po
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    px = np.load(tmp_path / "px.npy")
+    acc = np.load(tmp_path / "acc.npy")
+    total_segs, slowest = np.load(tmp_path / "meta.npy")
+    ref_px, ref_acc, ref_segs, _ = po.MeshScene(scenes.cornell34(), W, H).frames(0, SPP, DEPTH, nthreads=1)
+    assert np.array_equal(px, ref_px)
+    assert acc.tobytes() == ref_acc.tobytes()
+    assert int(total_segs) == ref_segs
+    assert slowest == float(world)
+
+
+def test_row_band_partition_covers_image():
+    for world in (1, 2, 3, 4, 8):
+        for h in (1, 7, 1080, 2160):
+            bands = [hd.row_band(r, world, h) for r in range(world)]
+            assert bands[0][0] == 0 and bands[-1][1] == h
+            assert all(bands[i][1] == bands[i + 1][0] for i in range(world - 1))
+    with pytest.raises(ValueError):
+        hd.row_band(2, 2, 10)
+
+
+def test_gather_without_process_group_is_identity():
+    a = np.arange(12, dtype=np.uint32).reshape(3, 4)
+    assert hd.gather_bands(a, 3) is a
+    assert hd.max_over_ranks(2.5) == 2.5 and hd.sum_over_ranks(7) == 7

@@ -17,7 +17,7 @@ sys.path.insert(0, os.path.join(REPO, "qt-raytracer_amd"))
 import hippt  # noqa: E402
 from hippt import scenes  # noqa: E402
 
-KEYS = {"wave": hippt.OPT_WAVE_THRESHOLD, "chunk": hippt.OPT_CHUNK}
+KEYS = {"wave": hippt.OPT_WAVE_THRESHOLD, "chunk": hippt.OPT_CHUNK, "lds": hippt.OPT_LDS_SCENE}
 
 
 def main():

@@ -21,7 +21,7 @@ import hippt  # noqa: E402
 from hippt import scenes  # noqa: E402
 
 KEYS = {"wave": hippt.OPT_WAVE_THRESHOLD, "chunk": hippt.OPT_CHUNK, "scratch": hippt.OPT_SCRATCH_MB,
-        "bpc": hippt.OPT_BLOCKS_PER_CU}
+        "bpc": hippt.OPT_BLOCKS_PER_CU, "lds": hippt.OPT_LDS_SCENE}
 
 
 def main():
