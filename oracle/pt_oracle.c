@@ -103,12 +103,26 @@ void po_camera_build(const double lookfrom[3], const double lookat[3], const dou
     out->pad_ = 0.0f;
 }
 
+/* Rejection-loop escape.  hash32 is a bijection with short cycles (fixed points 0 and
+ * 3496737362, the 2-cycle {160893342, 357741884}, a 5-cycle, ...); a seed on one of them on
+ * which every candidate is rejected makes the reference's `while (true)` loops
+ * (CudaPathTracerKernel.cu:61-68, RayTracer.h:155-169) spin forever — e.g. pixel
+ * (1750, 1610), frame 17 of a 3840x2160 image seeds the 2-cycle.  Contract: after every 64
+ * consecutive rejections the state is xored with PO_ESCAPE (a legitimate sequence is
+ * rejected 64 times with probability < 0.48^64 ~ 4e-21, so the first 64 attempts are
+ * exactly the reference's). */
+#define PO_ESCAPE 0x9E3779B9u
+#define PO_ESCAPE_EVERY 64
+
 /* random_in_unit_disk — RayTracer.h:163-169; random_double(-1,1) = -1 + 2r (:53-55). */
 void po_random_in_unit_disk(uint32_t *state, float p[3]) {
-    for (;;) {
+    for (unsigned tries = 1;; ++tries) {
         float x = fmaf(2.0f, po_rand01(state), -1.0f);
         float y = fmaf(2.0f, po_rand01(state), -1.0f);
-        if (fmaf(x, x, y * y) >= 1.0f) continue;
+        if (fmaf(x, x, y * y) >= 1.0f) {
+            if (tries % PO_ESCAPE_EVERY == 0) *state ^= PO_ESCAPE;
+            continue;
+        }
         p[0] = x; p[1] = y; p[2] = 0.0f;
         return;
     }
@@ -117,11 +131,14 @@ void po_random_in_unit_disk(uint32_t *state, float p[3]) {
 /* random_in_unit_sphere — RayTracer.h:155-161 (x, y, z drawn in that order, as
  * CudaPathTracerKernel.cu:63). */
 void po_random_in_unit_sphere(uint32_t *state, float p[3]) {
-    for (;;) {
+    for (unsigned tries = 1;; ++tries) {
         float x = fmaf(2.0f, po_rand01(state), -1.0f);
         float y = fmaf(2.0f, po_rand01(state), -1.0f);
         float z = fmaf(2.0f, po_rand01(state), -1.0f);
-        if (fmaf(x, x, fmaf(y, y, z * z)) >= 1.0f) continue;
+        if (fmaf(x, x, fmaf(y, y, z * z)) >= 1.0f) {
+            if (tries % PO_ESCAPE_EVERY == 0) *state ^= PO_ESCAPE;
+            continue;
+        }
         p[0] = x; p[1] = y; p[2] = z;
         return;
     }
@@ -266,13 +283,14 @@ static po_v3 s4_normalize(po_v3 v) { /* :53-59 */
     return v3(v.x / len, v.y / len, v.z / len);
 }
 
-static po_v3 s4_rius(uint32_t *st) { /* :61-68 */
-    for (;;) {
+static po_v3 s4_rius(uint32_t *st) { /* :61-68, plus the short-cycle escape (PO_ESCAPE) */
+    for (unsigned tries = 1;; ++tries) {
         float x = po_rand01(st) * 2.0f - 1.0f;
         float y = po_rand01(st) * 2.0f - 1.0f;
         float z = po_rand01(st) * 2.0f - 1.0f;
         po_v3 p = v3(x, y, z);
         if (pdot(p, p) < 1.0f) return p;
+        if (tries % PO_ESCAPE_EVERY == 0) *st ^= PO_ESCAPE;
     }
 }
 
@@ -483,6 +501,8 @@ static int build_rec(po_scene *sc, po_prim *prims, int begin, int end, float pad
 po_scene *po_scene_create(const float *verts, const int *tri_mat, int ntris, const float *albedo, int nmat,
                           const po_camera *cam, int accel) {
     po_scene *sc = (po_scene *)calloc(1, sizeof(po_scene));
+    if (ntris < 0) ntris = 0;
+    if (nmat < 0) nmat = 0;
     sc->ntris = ntris;
     sc->nmat = nmat;
     sc->cam = *cam;

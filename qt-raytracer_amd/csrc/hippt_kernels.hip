@@ -48,6 +48,13 @@ __device__ __forceinline__ float rand01(uint32_t &s) {
     return float(s) * 0x1p-32f;
 }
 
+// Rejection loops leave a short RNG cycle: after every 64 consecutive rejections the state is
+// xored with 0x9E3779B9 (pt_oracle.c PO_ESCAPE; the reference loops forever there, e.g. on
+// the 2-cycle {160893342, 357741884} seeded by pixel (1750,1610) frame 17 at 3840x2160).
+__device__ __forceinline__ void escape_cycle(uint32_t &s, unsigned tries) {
+    if ((tries & 63u) == 0u) s ^= 0x9E3779B9u;
+}
+
 // CudaPathTracerKernel.cu:144 in uint32 wrap-around.
 __device__ __forceinline__ uint32_t pixel_seed(uint32_t x, uint32_t y, uint32_t w, uint32_t f) {
     return (x + y * w) * 9781u + (f + 1u) * 6271u;
@@ -101,13 +108,14 @@ __device__ __forceinline__ V3 normalize3(V3 v) {  // :53-59
     return mk(v.x / len, v.y / len, v.z / len);
 }
 
-__device__ __forceinline__ V3 rius_legacy(uint32_t &st) {  // :61-68
-    for (;;) {
+__device__ __forceinline__ V3 rius_legacy(uint32_t &st) {  // :61-68 + short-cycle escape
+    for (unsigned tries = 1;; ++tries) {
         float x = rand01(st) * 2.0f - 1.0f;
         float y = rand01(st) * 2.0f - 1.0f;
         float z = rand01(st) * 2.0f - 1.0f;
         V3 p = mk(x, y, z);
         if (dot(p, p) < 1.0f) return p;
+        escape_cycle(st, tries);
     }
 }
 
@@ -328,10 +336,11 @@ __global__ __launch_bounds__(kMeshBlock, HIPPT_MESH_WAVES_PER_EU) void mesh_kern
                     const float s = (float(x) + rand01(rng)) * P.invW;
                     const float t = (float(y) + rand01(rng)) * P.invH;
                     float qx, qy;
-                    for (;;) {  // random_in_unit_disk, RayTracer.h:163-169
+                    for (unsigned tries = 1;; ++tries) {  // random_in_unit_disk, RayTracer.h:163-169
                         qx = fmaf(2.0f, rand01(rng), -1.0f);
                         qy = fmaf(2.0f, rand01(rng), -1.0f);
                         if (fmaf(qx, qx, qy * qy) < 1.0f) break;
+                        escape_cycle(rng, tries);
                     }
                     const CameraF &C = P.cam;
                     const float rx = C.lens_radius * qx, ry = C.lens_radius * qy;
@@ -464,13 +473,14 @@ __global__ __launch_bounds__(kMeshBlock, HIPPT_MESH_WAVES_PER_EU) void mesh_kern
                     nz = -nz;
                 }
                 float rx, ry, rz, r2;
-                for (;;) {  // random_in_unit_sphere, :155-161
+                for (unsigned tries = 1;; ++tries) {  // random_in_unit_sphere, :155-161
                     HIPPT_PROF(7);
                     rx = fmaf(2.0f, rand01(rng), -1.0f);
                     ry = fmaf(2.0f, rand01(rng), -1.0f);
                     rz = fmaf(2.0f, rand01(rng), -1.0f);
                     r2 = fmaf(rx, rx, fmaf(ry, ry, rz * rz));
                     if (r2 < 1.0f) break;
+                    escape_cycle(rng, tries);
                 }
                 const float inv = 1.0f / sqrtf(r2);  // unit_vector = (1/len)*v, :137-139,151-153
                 float sx = nx + rx * inv, sy = ny + ry * inv, sz = nz + rz * inv;
