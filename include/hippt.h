@@ -130,10 +130,12 @@ int hipptGetCounters(unsigned long long *out, int n);
 enum {
     HIPPT_OPT_COUNT_TRAVERSAL = 1,  /* 1: count node visits / triangle tests (slower) */
     HIPPT_OPT_WAVE_THRESHOLD = 2,   /* lanes still traversing below which a wave goes to shade */
-    HIPPT_OPT_SCRATCH_MB = 3,       /* cap of the per-batch sample scratch per device */
+    HIPPT_OPT_SCRATCH_MB = 3,       /* cap of the per-batch sample scratch per device (4096) */
     HIPPT_OPT_CHUNK = 4,            /* work items a wave takes from the global queue at once */
     HIPPT_OPT_BLOCKS_PER_CU = 5,    /* persistent-grid residency (0 = occupancy query) */
-    HIPPT_OPT_LDS_SCENE = 6         /* 1 (default): small scenes are copied into LDS per block */
+    HIPPT_OPT_LDS_SCENE = 6,        /* 1 (default): small scenes are copied into LDS per block */
+    HIPPT_OPT_PATH_MODE = 8,        /* 0 (default): persistent megakernel; 1: wavefront kernels */
+    HIPPT_OPT_WAVEFRONT_SLOTS = 9   /* wavefront path-state slots per device (default 2^24) */
 };
 bool hipptSetOption(int key, long long value);
 long long hipptGetOption(int key);

@@ -23,6 +23,7 @@
 
 #include "bvh_builder.h"
 #include "hippt_device.h"
+#include "hippt_wavefront.h"
 
 struct hipptBvh {
     hippt::Bvh bvh;
@@ -50,6 +51,13 @@ struct Ctx {
     unsigned long long *stats = nullptr;
     int sceneVersion = -1;
     float4 *nodes = nullptr, *tris = nullptr, *shade = nullptr, *albedo = nullptr;
+    // wavefront path-state pool (allocated on first use)
+    void *wfPool = nullptr;
+    unsigned wfSlots = 0;
+    unsigned *wfCtr = nullptr;
+    unsigned *wfHost = nullptr;  // pinned: two snapshots of the ray-queue shard counters
+    hipEvent_t wfPoll[2] = {nullptr, nullptr};
+    int wfOccKey = -1, wfBlocksPerCu[2] = {0, 0};
     int cus = 0;
     int occDepth = -1, meshBlocksPerCu[2] = {0, 0};  // occupancy cached per stack depth
     std::vector<EventPair> pool;                         // reusable events
@@ -82,10 +90,13 @@ struct State {
     // options
     bool countTraversal = false;
     int waveThreshold = 32;
-    long long scratchMB = 256;
+    // one batch (and one end-of-batch tail) per 1080p/64-spp call: 132.7M samples x 12 B
+    long long scratchMB = 4096;
     unsigned chunk = 256;
     int blocksPerCu = 0;
     bool ldsScene = true;
+    int pathMode = 0;             // 0 megakernel, 1 wavefront
+    unsigned wfSlots = 1u << 24;  // wavefront path-state slots per device
     // host-side timing accumulators
     double traceMs = 0, combineMs = 0;
     int traceLaunches = 0, combineLaunches = 0;
@@ -180,6 +191,11 @@ void destroy_ctx(Ctx &c) {
     (void)hipFree(c.scratch);
     (void)hipFree(c.queue);
     (void)hipFree(c.stats);
+    (void)hipFree(c.wfPool);
+    (void)hipFree(c.wfCtr);
+    (void)hipHostFree(c.wfHost);
+    for (hipEvent_t e : c.wfPoll)
+        if (e) (void)hipEventDestroy(e);
     free_scene_buffers(c);
     for (auto &e : c.pool) {
         (void)hipEventDestroy(e.a);
@@ -273,6 +289,81 @@ bool init_locked(int width, int height, const char **err) {
     if (init_inner(width, height, err)) return true;
     destroy_all();
     return false;
+}
+
+// Wavefront variant (hippt_wavefront.hip): init + generate, then extend/shade/generate
+// iterations until the ray queue stays empty.  The host reads the queue size with one batch of
+// lag (pinned snapshot + event), so the call returns within ~16 iterations of the end.
+bool run_wavefront(Ctx &c, const hippt::MeshParams &p, bool cnt, const char **err) {
+    State &s = S();
+    const unsigned slots = std::max(64u, std::min(s.wfSlots, std::max(64u, p.totalItems)));
+    unsigned shardCap = 0;
+    const size_t words = hippt::wf_pool_words(slots, &shardCap);
+    if (c.wfSlots != slots || !c.wfPool) {
+        HIP_TRY(hipStreamSynchronize(c.stream));
+        (void)hipFree(c.wfPool);
+        c.wfPool = nullptr;
+        c.wfSlots = 0;
+        HIP_TRY(hipMalloc(&c.wfPool, words * sizeof(uint32_t)));
+        c.wfSlots = slots;
+    }
+    if (!c.wfCtr) HIP_TRY(hipMalloc(&c.wfCtr, hippt::kCtrWords * sizeof(unsigned)));
+    hippt::WfParams W{};
+    W.mp = p;
+    W.slots = slots;
+    W.shardCap = shardCap;
+    W.ctr = c.wfCtr;
+    auto *base = static_cast<uint32_t *>(c.wfPool);
+    // slot records, then 3 sharded queues
+    W.st = reinterpret_cast<float4 *>(base);
+    uint32_t *queues = base + size_t(hippt::kWfStateWords) * slots;
+    W.extQ0 = queues;
+    W.extQ1 = queues + size_t(hippt::kWfShards) * shardCap;
+    W.genQ = queues + 2 * size_t(hippt::kWfShards) * shardCap;
+    const int occKey = p.stackDepth * 2 + (p.ldsScene ? 1 : 0);
+    if (c.wfOccKey != occKey) {
+        const int ln = p.ldsScene ? p.numNodes : 0, lt = p.ldsScene ? p.numTris : 0;
+        c.wfBlocksPerCu[0] = hippt::wf_extend_blocks_per_cu(false, p.stackDepth, ln, lt);
+        c.wfBlocksPerCu[1] = hippt::wf_extend_blocks_per_cu(true, p.stackDepth, ln, lt);
+        c.wfOccKey = occKey;
+    }
+    const int bpc = s.blocksPerCu > 0 ? s.blocksPerCu : c.wfBlocksPerCu[cnt ? 1 : 0];
+    const int blocks = int(std::max(1LL, std::min<long long>((long long)c.cus * bpc, (slots + 255) / 256)));
+    EventPair ev;
+    if (!next_events(c, ev, err)) return false;
+    HIP_TRY(hipEventRecord(ev.a, c.stream));
+    HIP_TRY(hippt::wf_launch_init(W, c.stream));
+    HIP_TRY(hippt::wf_launch_generate(W, 0, false, c.stream));
+    // every path needs <= maxDepth extend rounds; slots regenerate as paths end
+    const long long maxIter = (long long)p.maxDepth * ((p.totalItems + slots - 1) / slots + 1) + 64;
+    // Every kPollEvery iterations the ray-queue sizes are copied to pinned memory; the host
+    // reads the snapshot one batch later, so the stream always holds a batch of queued work.
+    // Iterations after the queue drained are no-ops (empty queues).
+    constexpr int kPollEvery = 8, kSnap = hippt::kWfShards * hippt::kCtrStride;
+    if (!c.wfHost) HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c.wfHost), 2 * kSnap * sizeof(unsigned)));
+    for (hipEvent_t &e : c.wfPoll)
+        if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    int cur = 0;
+    for (long long it = 0;; ++it) {
+        if (it > maxIter) return fail(err, "wavefront path tracer did not drain its ray queue");
+        HIP_TRY(hippt::wf_launch_extend(W, cur, blocks, cnt, c.stream));
+        HIP_TRY(hippt::wf_launch_shade(W, cur, c.stream));
+        HIP_TRY(hippt::wf_launch_generate(W, cur ^ 1, true, c.stream));
+        cur ^= 1;
+        if (it % kPollEvery != kPollEvery - 1) continue;
+        const int b = int(it / kPollEvery) & 1;
+        HIP_TRY(hipMemcpyAsync(c.wfHost + b * kSnap, c.wfCtr + hippt::ctr_word(hippt::kCtrExt0 + cur * hippt::kWfShards),
+                               kSnap * sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
+        HIP_TRY(hipEventRecord(c.wfPoll[b], c.stream));
+        if (it < 2 * kPollEvery - 1) continue;
+        HIP_TRY(hipEventSynchronize(c.wfPoll[b ^ 1]));
+        unsigned left = 0;
+        for (int k = 0; k < hippt::kWfShards; ++k) left += c.wfHost[(b ^ 1) * kSnap + k * hippt::kCtrStride];
+        if (left == 0) break;
+    }
+    HIP_TRY(hipEventRecord(ev.b, c.stream));
+    c.pending.push_back({0, ev});
+    return true;
 }
 
 CameraF current_camera() {
@@ -370,16 +461,20 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.ldsScene = ldsScene ? 1 : 0;
                         p.waveThreshold = s.waveThreshold;
                         p.chunk = s.chunk;
-                        long long blocks = (long long)c.cus * bpc;
-                        blocks = std::min<long long>(blocks, (total + hippt::kMeshBlock - 1) / hippt::kMeshBlock);
-                        blocks = std::max<long long>(blocks, 1);
-                        HIP_TRY(hipMemsetAsync(c.queue, 0, sizeof(unsigned), c.stream));
-                        EventPair ev;
-                        if (!next_events(c, ev, err)) return false;
-                        HIP_TRY(hipEventRecord(ev.a, c.stream));
-                        HIP_TRY(hippt::launch_mesh(p, int(blocks), cnt, c.stream));
-                        HIP_TRY(hipEventRecord(ev.b, c.stream));
-                        c.pending.push_back({0, ev});
+                        if (s.pathMode == 1) {
+                            if (!run_wavefront(c, p, cnt, err)) return false;
+                        } else {
+                            long long blocks = (long long)c.cus * bpc;
+                            blocks = std::min<long long>(blocks, (total + hippt::kMeshBlock - 1) / hippt::kMeshBlock);
+                            blocks = std::max<long long>(blocks, 1);
+                            HIP_TRY(hipMemsetAsync(c.queue, 0, sizeof(unsigned), c.stream));
+                            EventPair ev;
+                            if (!next_events(c, ev, err)) return false;
+                            HIP_TRY(hipEventRecord(ev.a, c.stream));
+                            HIP_TRY(hippt::launch_mesh(p, int(blocks), cnt, c.stream));
+                            HIP_TRY(hipEventRecord(ev.b, c.stream));
+                            c.pending.push_back({0, ev});
+                        }
                     }
                     hippt::CombineParams q{c.accum, c.out, c.scratch, bandPixels, total, firstFrame + b, nf};
                     EventPair ev2;
@@ -696,6 +791,14 @@ extern "C" bool hipptSetOption(int key, long long value) {
         s.blocksPerCu = int(value);
         return true;
     case HIPPT_OPT_LDS_SCENE: s.ldsScene = value != 0; return true;
+    case HIPPT_OPT_PATH_MODE:
+        if (value != 0 && value != 1) return false;
+        s.pathMode = int(value);
+        return true;
+    case HIPPT_OPT_WAVEFRONT_SLOTS:
+        if (value < 64 || value > (1LL << 26)) return false;
+        s.wfSlots = unsigned(value);
+        return true;
     default: return false;
     }
 }
@@ -710,6 +813,8 @@ extern "C" long long hipptGetOption(int key) {
     case HIPPT_OPT_CHUNK: return s.chunk;
     case HIPPT_OPT_BLOCKS_PER_CU: return s.blocksPerCu;
     case HIPPT_OPT_LDS_SCENE: return s.ldsScene ? 1 : 0;
+    case HIPPT_OPT_PATH_MODE: return s.pathMode;
+    case HIPPT_OPT_WAVEFRONT_SLOTS: return s.wfSlots;
     default: return -1;
     }
 }

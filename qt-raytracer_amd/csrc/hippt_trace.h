@@ -1,0 +1,289 @@
+// hippt_trace.h — device building blocks of the triangle path tracer shared by the wavefront
+// kernels (hippt_wavefront.hip).  Same arithmetic contract as hippt_kernels.hip and
+// oracle/pt_oracle.c: -ffp-contract=off, FMAs only where written, IEEE division/sqrt.
+#pragma once
+
+#include "bvh_builder.h"
+#include "hippt_device.h"
+
+#pragma clang fp contract(off)
+
+namespace hippt {
+namespace trace {
+
+constexpr unsigned kNone = 0xffffffffu;
+constexpr int kDone = int(0x80000000);
+
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {  // CudaPathTracerKernel.cu:23-30
+    x ^= x >> 16;
+    x *= 0x7feb352du;
+    x ^= x >> 15;
+    x *= 0x846ca68bu;
+    x ^= x >> 16;
+    return x;
+}
+
+__device__ __forceinline__ float rand01(uint32_t &s) {  // :32-35 (÷4294967295.0f == ×2^-32)
+    s = hash32(s);
+    return float(s) * 0x1p-32f;
+}
+
+// Short-cycle escape of the rejection loops (pt_oracle.c PO_ESCAPE).
+__device__ __forceinline__ void escape_cycle(uint32_t &s, unsigned tries) {
+    if ((tries & 63u) == 0u) s ^= 0x9E3779B9u;
+}
+
+__device__ __forceinline__ uint32_t pixel_seed(uint32_t x, uint32_t y, uint32_t w, uint32_t f) {
+    return (x + y * w) * 9781u + (f + 1u) * 6271u;  // :144, uint32 wrap-around
+}
+
+__device__ __forceinline__ float fdot(float ax, float ay, float az, float bx, float by, float bz) {
+    return fmaf(ax, bx, fmaf(ay, by, az * bz));
+}
+
+__device__ __forceinline__ void divmod(unsigned n, unsigned d, float rcp, unsigned &q, unsigned &r) {
+    q = unsigned(float(n) * rcp);
+    int rem = int(n - q * d);
+    if (rem < 0) {
+        --q;
+        rem += int(d);
+    } else if (rem >= int(d)) {
+        ++q;
+        rem -= int(d);
+    }
+    r = unsigned(rem);
+}
+
+__device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+    return v;
+}
+
+// Wave-pooled grab from a global counter (see hippt_kernels.hip wave_fetch).  Whole wave,
+// uniform control flow.
+__device__ __forceinline__ unsigned wave_fetch(bool req, unsigned &poolNext, unsigned &poolEnd, unsigned *queue,
+                                               unsigned chunk, unsigned total) {
+    const unsigned long long mask = __ballot(req);
+    const unsigned n = unsigned(__popcll(mask));
+    const unsigned rank = __builtin_amdgcn_mbcnt_hi(unsigned(mask >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(mask), 0u));
+    const unsigned avail = poolEnd - poolNext;
+    unsigned item;
+    if (n <= avail) {
+        item = poolNext + rank;
+        poolNext += n;
+    } else {
+        unsigned base = 0;
+        if (__lane_id() == 0) base = atomicAdd(queue, chunk);
+        base = __builtin_amdgcn_readfirstlane(base);
+        item = rank < avail ? poolNext + rank : base + (rank - avail);
+        poolNext = base + (n - avail);
+        poolEnd = base + chunk;
+    }
+    return (req && item < total) ? item : kNone;
+}
+
+// Wave-aggregated append of one entry per requesting lane to queue[] (one atomic per wave).
+__device__ __forceinline__ void wave_append(bool req, unsigned value, unsigned *queue, unsigned *count) {
+    const unsigned long long mask = __ballot(req);
+    if (!mask) return;
+    const unsigned n = unsigned(__popcll(mask));
+    const unsigned rank = __builtin_amdgcn_mbcnt_hi(unsigned(mask >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(mask), 0u));
+    const int leader = __ffsll((unsigned long long)mask) - 1;
+    unsigned base = 0;
+    if (int(__lane_id()) == leader) base = atomicAdd(count, n);
+    base = __builtin_amdgcn_readlane(base, leader);
+    if (req) queue[base + rank] = value;
+}
+
+struct Ray {
+    float ox, oy, oz, dx, dy, dz;
+    float ix, iy, iz, oix, oiy, oiz;  // box-test reciprocals (fast rcp; not result-defining)
+};
+
+__device__ __forceinline__ void prepare(Ray &r) {
+    const float cx = copysignf(fmaxf(fabsf(r.dx), 1e-20f), r.dx);
+    const float cy = copysignf(fmaxf(fabsf(r.dy), 1e-20f), r.dy);
+    const float cz = copysignf(fmaxf(fabsf(r.dz), 1e-20f), r.dz);
+    r.ix = __builtin_amdgcn_rcpf(cx);
+    r.iy = __builtin_amdgcn_rcpf(cy);
+    r.iz = __builtin_amdgcn_rcpf(cz);
+    r.oix = r.ox * r.ix;
+    r.oiy = r.oy * r.iy;
+    r.oiz = r.oz * r.iz;
+}
+
+// Camera sample for work item `it`: RenderWorker::render u/v (RayTracerFboItem.cpp:109-110) and
+// Camera::get_ray (RayTracer.h:563-567, disk draw always consumed).
+__device__ __forceinline__ void camera_sample(const MeshParams &P, unsigned it, Ray &r, uint32_t &rng) {
+    unsigned fl, p, yb, x;
+    divmod(it, P.bandPixels, P.rcpBandPixels, fl, p);
+    divmod(p, unsigned(P.width), P.rcpWidth, yb, x);
+    const unsigned y = unsigned(P.y0) + yb;
+    rng = pixel_seed(x, y, unsigned(P.width), unsigned(P.firstFrame) + fl);
+    const float s = (float(x) + rand01(rng)) * P.invW;
+    const float t = (float(y) + rand01(rng)) * P.invH;
+    float qx, qy;
+    for (unsigned tries = 1;; ++tries) {  // random_in_unit_disk, RayTracer.h:163-169
+        qx = fmaf(2.0f, rand01(rng), -1.0f);
+        qy = fmaf(2.0f, rand01(rng), -1.0f);
+        if (fmaf(qx, qx, qy * qy) < 1.0f) break;
+        escape_cycle(rng, tries);
+    }
+    const CameraF &C = P.cam;
+    const float rx = C.lens_radius * qx, ry = C.lens_radius * qy;
+    const float fx = fmaf(C.v[0], ry, C.u[0] * rx);
+    const float fy = fmaf(C.v[1], ry, C.u[1] * rx);
+    const float fz = fmaf(C.v[2], ry, C.u[2] * rx);
+    r.ox = C.origin[0] + fx;
+    r.oy = C.origin[1] + fy;
+    r.oz = C.origin[2] + fz;
+    r.dx = (fmaf(t, C.vertical[0], fmaf(s, C.horizontal[0], C.llc[0])) - C.origin[0]) - fx;
+    r.dy = (fmaf(t, C.vertical[1], fmaf(s, C.horizontal[1], C.llc[1])) - C.origin[1]) - fy;
+    r.dz = (fmaf(t, C.vertical[2], fmaf(s, C.horizontal[2], C.llc[2])) - C.origin[2]) - fz;
+}
+
+// Sky gradient on a miss (RayTracer.h:593-595), times throughput.
+__device__ __forceinline__ void sky(const Ray &r, float tr, float tg, float tb, float &L0, float &L1, float &L2) {
+    const float uy = (1.0f / sqrtf(fdot(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz))) * r.dy;
+    const float al = 0.5f * (uy + 1.0f);
+    const float bl = 1.0f - al;
+    L0 = tr * fmaf(al, 0.5f, bl);
+    L1 = tg * fmaf(al, 0.7f, bl);
+    L2 = tb * fmaf(al, 1.0f, bl);
+}
+
+// Lambertian scatter at hit (t, shading record sh): ray_color / Lambertian::scatter
+// (RayTracer.h:585-589, :477-484), throughput *= albedo.
+__device__ __forceinline__ void scatter(Ray &r, float t, float4 sh, const float4 *albedo, uint32_t &rng, float &tr,
+                                        float &tg, float &tb) {
+    float nx = sh.x, ny = sh.y, nz = sh.z;
+    const float px = fmaf(t, r.dx, r.ox), py = fmaf(t, r.dy, r.oy), pz = fmaf(t, r.dz, r.oz);
+    if (!(fdot(r.dx, r.dy, r.dz, nx, ny, nz) < 0.0f)) {  // set_face_normal, :215-218
+        nx = -nx;
+        ny = -ny;
+        nz = -nz;
+    }
+    float rx, ry, rz, r2;
+    for (unsigned tries = 1;; ++tries) {  // random_in_unit_sphere, :155-161
+        rx = fmaf(2.0f, rand01(rng), -1.0f);
+        ry = fmaf(2.0f, rand01(rng), -1.0f);
+        rz = fmaf(2.0f, rand01(rng), -1.0f);
+        r2 = fmaf(rx, rx, fmaf(ry, ry, rz * rz));
+        if (r2 < 1.0f) break;
+        escape_cycle(rng, tries);
+    }
+    const float inv = 1.0f / sqrtf(r2);
+    float sx = nx + rx * inv, sy = ny + ry * inv, sz = nz + rz * inv;
+    if (fdot(sx, sy, sz, sx, sy, sz) < 1e-8f) {
+        sx = nx;
+        sy = ny;
+        sz = nz;
+    }
+    const float4 alb = albedo[__float_as_int(sh.w)];
+    tr *= alb.x;
+    tg *= alb.y;
+    tb *= alb.z;
+    r.ox = px;
+    r.oy = py;
+    r.oz = pz;
+    r.dx = sx;
+    r.dy = sy;
+    r.dz = sz;
+}
+
+struct Trav {
+    int cur;    // next node (>= 0), leaf code (< 0), or kDone
+    int sp;     // stack depth * kMeshBlock
+    int leaf;   // postponed leaf code or 0
+    float bestT;
+    int bestI, bestO;
+};
+
+__device__ __forceinline__ void begin(Trav &T) {
+    T.cur = 0;
+    T.sp = 0;
+    T.leaf = 0;
+    T.bestT = INFINITY;
+    T.bestI = -1;
+    T.bestO = 0x7fffffff;
+}
+
+// One speculative while-while round (Aila & Laine 2009) over the BVH: interior loop until
+// every lane still in it holds a postponed leaf, then the leaf loop.  `my` = this lane's
+// LDS stack column (entry k at my[k*kMeshBlock]).  Closest hit = min (t, original index).
+template <int NODE_F4>
+__device__ __forceinline__ void traverse_round(Trav &T, const Ray &r, int *my, const float4 *nodes,
+                                               const float4 *tris, unsigned &nvis, unsigned &ntest) {
+    const float tmin = 0.001f;
+    while (T.cur >= 0) {
+        const float4 *nd = nodes + __umul24(unsigned(T.cur), unsigned(NODE_F4));
+        const float4 a = nd[0], b = nd[1], c = nd[2];
+        const int4 e = *reinterpret_cast<const int4 *>(nd + 3);
+        ++nvis;
+        const float l0x = fmaf(a.x, r.ix, -r.oix), h0x = fmaf(a.w, r.ix, -r.oix);
+        const float l0y = fmaf(a.y, r.iy, -r.oiy), h0y = fmaf(b.x, r.iy, -r.oiy);
+        const float l0z = fmaf(a.z, r.iz, -r.oiz), h0z = fmaf(b.y, r.iz, -r.oiz);
+        const float l1x = fmaf(b.z, r.ix, -r.oix), h1x = fmaf(c.y, r.ix, -r.oix);
+        const float l1y = fmaf(b.w, r.iy, -r.oiy), h1y = fmaf(c.z, r.iy, -r.oiy);
+        const float l1z = fmaf(c.x, r.iz, -r.oiz), h1z = fmaf(c.w, r.iz, -r.oiz);
+        const float n0 = fmaxf(fmaxf(fminf(l0x, h0x), fminf(l0y, h0y)), fmaxf(fminf(l0z, h0z), tmin));
+        const float f0 = fminf(fminf(fmaxf(l0x, h0x), fmaxf(l0y, h0y)), fminf(fmaxf(l0z, h0z), T.bestT));
+        const float n1 = fmaxf(fmaxf(fminf(l1x, h1x), fminf(l1y, h1y)), fmaxf(fminf(l1z, h1z), tmin));
+        const float f1 = fminf(fminf(fmaxf(l1x, h1x), fmaxf(l1y, h1y)), fminf(fmaxf(l1z, h1z), T.bestT));
+        const bool hit0 = n0 <= f0, hit1 = n1 <= f1;
+        const bool take0 = hit0 & (!hit1 | (n0 <= n1));
+        const int nearC = take0 ? e.x : e.y;
+        const int farC = take0 ? e.y : e.x;
+        my[T.sp] = farC;
+        const int top = my[max(T.sp - kMeshBlock, 0)];
+        const bool none = !(hit0 || hit1);
+        T.sp += (hit0 && hit1) ? kMeshBlock : 0;
+        T.cur = none ? (T.sp > 0 ? top : kDone) : nearC;
+        T.sp -= (none && T.sp > 0) ? kMeshBlock : 0;
+        if (T.cur < 0 && T.cur != kDone && T.leaf == 0) {
+            T.leaf = T.cur;
+            T.cur = T.sp > 0 ? my[T.sp -= kMeshBlock] : kDone;
+        }
+        if (!__any(T.leaf == 0)) break;
+    }
+    while (T.leaf != 0) {
+        const int code = ~T.leaf;
+        const int first = code >> 4, last = first + (code & 15);
+        for (int i = first; i < last; ++i) {
+            const float4 *tp = tris + 3 * i;
+            const float4 A = tp[0], B = tp[1], Cc = tp[2];
+            ++ntest;
+            const float e1x = A.w, e1y = B.x, e1z = B.y;
+            const float e2x = B.z, e2y = B.w, e2z = Cc.x;
+            const float pvx = fmaf(r.dy, e2z, -(r.dz * e2y));
+            const float pvy = fmaf(r.dz, e2x, -(r.dx * e2z));
+            const float pvz = fmaf(r.dx, e2y, -(r.dy * e2x));
+            const float det = fdot(e1x, e1y, e1z, pvx, pvy, pvz);
+            const float tvx = r.ox - A.x, tvy = r.oy - A.y, tvz = r.oz - A.z;
+            const float un = fdot(tvx, tvy, tvz, pvx, pvy, pvz);
+            const float qvx = fmaf(tvy, e1z, -(tvz * e1y));
+            const float qvy = fmaf(tvz, e1x, -(tvx * e1z));
+            const float qvz = fmaf(tvx, e1y, -(tvy * e1x));
+            const float vn = fdot(r.dx, r.dy, r.dz, qvx, qvy, qvz);
+            const bool neg = det < 0.0f;
+            const float us = neg ? -un : un, vs = neg ? -vn : vn;
+            if (det != 0.0f && us >= 0.0f && vs >= 0.0f && us + vs <= fabsf(det)) {
+                const float tt = fdot(e2x, e2y, e2z, qvx, qvy, qvz) / det;
+                const int orig = __float_as_int(Cc.y);
+                if (tt >= tmin && (tt < T.bestT || (tt == T.bestT && orig < T.bestO))) {
+                    T.bestT = tt;
+                    T.bestI = i;
+                    T.bestO = orig;
+                }
+            }
+        }
+        T.leaf = 0;
+        if (T.cur < 0 && T.cur != kDone) {
+            T.leaf = T.cur;
+            T.cur = T.sp > 0 ? my[T.sp -= kMeshBlock] : kDone;
+        }
+    }
+}
+
+}  // namespace trace
+}  // namespace hippt

@@ -32,6 +32,8 @@ OPT_SCRATCH_MB = 3
 OPT_CHUNK = 4
 OPT_BLOCKS_PER_CU = 5
 OPT_LDS_SCENE = 6
+OPT_PATH_MODE = 8
+OPT_WAVEFRONT_SLOTS = 9
 
 # Every symbol include/hippt.h declares (checked by tests/test_abi_cpu.py).
 EXPORTS = (

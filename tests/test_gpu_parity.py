@@ -20,8 +20,9 @@ def pt():
     t.setDevices([])
     t.setRowRange(0, 0)
     t.useBuiltinScene(hippt.SCENE_SPHERE4)
-    for k, v in ((hippt.OPT_WAVE_THRESHOLD, 32), (hippt.OPT_SCRATCH_MB, 256), (hippt.OPT_CHUNK, 256),
-                 (hippt.OPT_COUNT_TRAVERSAL, 0), (hippt.OPT_BLOCKS_PER_CU, 0)):
+    for k, v in ((hippt.OPT_WAVE_THRESHOLD, 32), (hippt.OPT_SCRATCH_MB, 4096), (hippt.OPT_CHUNK, 256),
+                 (hippt.OPT_COUNT_TRAVERSAL, 0), (hippt.OPT_BLOCKS_PER_CU, 0), (hippt.OPT_LDS_SCENE, 1),
+                 (hippt.OPT_PATH_MODE, 0), (hippt.OPT_WAVEFRONT_SLOTS, 1 << 24)):
         t.setOption(k, v)
     t.resetStats()
     yield t
@@ -94,6 +95,43 @@ def test_mesh_matches_oracle(pt, name, w, h, spp, depth):
     _assert_same(px, acc, ora_px, ora_acc)
     st = pt.stats()
     assert st["segments"] == segs and st["pixelSamples"] == samples
+
+
+@pytest.mark.parametrize("name,w,h,spp,depth,slots", [
+    ("cornell34", 96, 64, 8, 8, 1 << 21),
+    ("cornell34", 33, 17, 3, 4, 64),
+    ("blob70k", 64, 48, 4, 8, 1000),
+    ("blob70k", 20, 11, 2, 1, 100),
+])
+def test_wavefront_matches_oracle(pt, name, w, h, spp, depth, slots):
+    """The wavefront variant (BASELINE config 5) is bit-identical to the oracle/megakernel,
+    including with a path pool much smaller than the work (many regenerate rounds)."""
+    sc = scenes.get_scene(name)
+    pt.uploadMesh(sc)
+    pt.setOption(hippt.OPT_PATH_MODE, 1)
+    pt.setOption(hippt.OPT_WAVEFRONT_SLOTS, slots)
+    assert pt.initialize(w, h), pt.lastError()
+    assert pt.renderFrames(spp, depth), pt.lastError()
+    px, acc = pt.readback()
+    ora_px, ora_acc, segs, samples = po.MeshScene(sc, w, h).frames(0, spp, depth)
+    _assert_same(px, acc, ora_px, ora_acc)
+    st = pt.stats()
+    assert st["segments"] == segs and st["pixelSamples"] == samples
+
+
+@pytest.mark.parametrize("slots", [1 << 21, 1 << 24])
+def test_wavefront_equals_megakernel_1080p(pt, slots):
+    """Full-width frames; 2^21 slots regenerate (shards refill unevenly), 2^24 hold every path."""
+    sc = scenes.blob70k()
+    pt.uploadMesh(sc)
+    pt.setOption(hippt.OPT_WAVEFRONT_SLOTS, slots)
+    got = []
+    for mode in (0, 1):
+        pt.setOption(hippt.OPT_PATH_MODE, mode)
+        assert pt.initialize(1920, 1080)
+        assert pt.renderFrames(2, 8)
+        got.append(pt.readback())
+    _assert_same(got[0][0], got[0][1], got[1][0], got[1][1])
 
 
 def test_mesh_wave_threshold_and_chunk_do_not_change_results(pt):

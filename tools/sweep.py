@@ -21,7 +21,8 @@ import hippt  # noqa: E402
 from hippt import scenes  # noqa: E402
 
 KEYS = {"wave": hippt.OPT_WAVE_THRESHOLD, "chunk": hippt.OPT_CHUNK, "scratch": hippt.OPT_SCRATCH_MB,
-        "bpc": hippt.OPT_BLOCKS_PER_CU, "lds": hippt.OPT_LDS_SCENE}
+        "bpc": hippt.OPT_BLOCKS_PER_CU, "lds": hippt.OPT_LDS_SCENE, "mode": hippt.OPT_PATH_MODE,
+        "slots": hippt.OPT_WAVEFRONT_SLOTS}
 
 
 def main():
