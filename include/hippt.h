@@ -75,6 +75,27 @@ bool hipptUploadMesh(const float *verts, const int *triMaterial, int numTris, co
                      int numMaterials, const double lookfrom[3], const double lookat[3], const double vup[3],
                      double vfovDeg, double aperture, double focusDist, const char **errorMessage);
 
+/* Materials of RayTracer.h :473-540.  LAMBERTIAN uses albedo; METAL albedo and fuzz (clamped
+ * to <= 1 as Metal's constructor does, :494); DIELECTRIC the index of refraction ir. */
+enum { HIPPT_MAT_LAMBERTIAN = 0, HIPPT_MAT_METAL = 1, HIPPT_MAT_DIELECTRIC = 2 };
+typedef struct {
+    int kind;
+    float albedo[3];
+    float fuzz;
+    float ir;
+} hipptMaterial;
+
+/* General scene: triangles (as hipptUploadMesh) plus spheres = numSpheres*4 floats (center
+ * xyz, radius; Sphere, RayTracer.h:274-322), each primitive with a material index into
+ * materials[numMaterials].  Either count may be 0, not both.  Ties of the closest hit are
+ * broken by primitive id: triangles 0..numTris-1, then spheres.  The reference app's scene
+ * (random_scene(), RayTracer.h:599-643, which draws from a nondeterministic RNG) is uploaded
+ * as its sphere list. */
+bool hipptUploadScene(const float *verts, const int *triMaterial, int numTris, const float *spheres,
+                      const int *sphereMaterial, int numSpheres, const hipptMaterial *materials, int numMaterials,
+                      const double lookfrom[3], const double lookat[3], const double vup[3], double vfovDeg,
+                      double aperture, double focusDist, const char **errorMessage);
+
 /* Optional: replace the camera by a prebuilt one (used as-is, whatever the aspect). */
 bool hipptSetCamera(const hipptCamera *camera, const char **errorMessage);
 

@@ -437,25 +437,29 @@ void po_sphere4_frames(int width, int height, int y0, int y1, int first_frame, i
 }
 
 /* ------------------------------------------------------------------------- */
-/* Mesh scene + oracle-private BVH (median split; result-identical to brute   */
-/* force because culling is conservative and ties break on original index)    */
+/* Scene: triangles + spheres + materials, and an oracle-private BVH (median   */
+/* split; result-identical to brute force because culling is conservative and  */
+/* ties break on the primitive id)                                             */
 /* ------------------------------------------------------------------------- */
 typedef struct {
     float lo[3], hi[3];
     int left, right; /* internal: children; leaf: left = first, right = -count */
 } po_node;
 
+typedef struct { po_v3 c; float r, r2; } po_sph;
+
 struct po_scene {
-    int ntris;
-    po_tri *tris;   /* in BVH leaf order when accel */
-    int *orig;      /* original index of tris[i] */
-    int *mat;       /* material of tris[i] */
+    int ntris, nsph, nprim; /* primitive id: triangles 0..ntris-1, then spheres */
+    po_tri *tris;           /* by triangle index */
+    po_sph *sph;            /* by sphere index */
+    int *prim_mat;          /* material of primitive id */
     int nmat;
-    float *albedo;
+    po_material *mats;
     po_camera cam;
     int accel;
     po_node *nodes;
     int nnodes;
+    int *ref; /* BVH leaf order -> primitive id */
 };
 
 typedef struct { float lo[3], hi[3], c[3]; int id; } po_prim;
@@ -498,60 +502,133 @@ static int build_rec(po_scene *sc, po_prim *prims, int begin, int end, float pad
     return ni;
 }
 
-po_scene *po_scene_create(const float *verts, const int *tri_mat, int ntris, const float *albedo, int nmat,
-                          const po_camera *cam, int accel) {
+static void *xmalloc(size_t n) { return malloc(n > 0 ? n : 1); }
+
+po_scene *po_scene_create2(const float *verts, const int *tri_mat, int ntris, const float *spheres,
+                           const int *sph_mat, int nsph, const po_material *mats, int nmat, const po_camera *cam,
+                           int accel) {
     po_scene *sc = (po_scene *)calloc(1, sizeof(po_scene));
     if (ntris < 0) ntris = 0;
+    if (nsph < 0) nsph = 0;
     if (nmat < 0) nmat = 0;
     sc->ntris = ntris;
+    sc->nsph = nsph;
+    sc->nprim = ntris + nsph;
     sc->nmat = nmat;
     sc->cam = *cam;
-    sc->accel = accel;
-    sc->albedo = (float *)malloc(sizeof(float) * 3 * (size_t)(nmat > 0 ? nmat : 1));
-    memcpy(sc->albedo, albedo, sizeof(float) * 3 * (size_t)nmat);
-    sc->tris = (po_tri *)malloc(sizeof(po_tri) * (size_t)(ntris > 0 ? ntris : 1));
-    sc->orig = (int *)malloc(sizeof(int) * (size_t)(ntris > 0 ? ntris : 1));
-    sc->mat = (int *)malloc(sizeof(int) * (size_t)(ntris > 0 ? ntris : 1));
-    if (!accel || ntris == 0) {
-        for (int i = 0; i < ntris; ++i) {
-            po_tri_setup(verts + 9 * (size_t)i, &sc->tris[i]);
-            sc->orig[i] = i;
-            sc->mat[i] = tri_mat[i];
-        }
-        sc->accel = 0;
-        return sc;
+    sc->accel = accel && sc->nprim > 0;
+    sc->mats = (po_material *)xmalloc(sizeof(po_material) * (size_t)nmat);
+    for (int m = 0; m < nmat; ++m) {
+        sc->mats[m] = mats[m];
+        /* Metal(a, f): fuzz(f < 1 ? f : 1), RayTracer.h:494 */
+        if (sc->mats[m].kind == PO_METAL && !(sc->mats[m].fuzz < 1.0f)) sc->mats[m].fuzz = 1.0f;
     }
-    po_prim *prims = (po_prim *)malloc(sizeof(po_prim) * (size_t)ntris);
-    float maxabs = fmaxf(fmaxf(fabsf(cam->origin.x), fabsf(cam->origin.y)), fabsf(cam->origin.z));
+    sc->tris = (po_tri *)xmalloc(sizeof(po_tri) * (size_t)ntris);
+    sc->sph = (po_sph *)xmalloc(sizeof(po_sph) * (size_t)nsph);
+    sc->prim_mat = (int *)xmalloc(sizeof(int) * (size_t)sc->nprim);
+    sc->ref = (int *)xmalloc(sizeof(int) * (size_t)sc->nprim);
     for (int i = 0; i < ntris; ++i) {
-        const float *v = verts + 9 * (size_t)i;
+        po_tri_setup(verts + 9 * (size_t)i, &sc->tris[i]);
+        sc->prim_mat[i] = tri_mat[i];
+    }
+    for (int j = 0; j < nsph; ++j) {
+        const float *q = spheres + 4 * (size_t)j;
+        sc->sph[j].c = v3(q[0], q[1], q[2]);
+        sc->sph[j].r = q[3];
+        sc->sph[j].r2 = q[3] * q[3];
+        sc->prim_mat[ntris + j] = sph_mat[j];
+    }
+    for (int i = 0; i < sc->nprim; ++i) sc->ref[i] = i;
+    if (!sc->accel) return sc;
+    po_prim *prims = (po_prim *)xmalloc(sizeof(po_prim) * (size_t)sc->nprim);
+    float maxabs = fmaxf(fmaxf(fabsf(cam->origin.x), fabsf(cam->origin.y)), fabsf(cam->origin.z));
+    for (int i = 0; i < sc->nprim; ++i) {
+        float mn[3], mx[3];
+        if (i < ntris) {
+            const float *v = verts + 9 * (size_t)i;
+            for (int a = 0; a < 3; ++a) {
+                mn[a] = fminf(fminf(v[a], v[3 + a]), v[6 + a]);
+                mx[a] = fmaxf(fmaxf(v[a], v[3 + a]), v[6 + a]);
+            }
+        } else {
+            const po_sph *q = &sc->sph[i - ntris];
+            float c[3] = {q->c.x, q->c.y, q->c.z}, r = fabsf(q->r) * (1.0f + 1.0f / 4096.0f);
+            for (int a = 0; a < 3; ++a) { mn[a] = c[a] - r; mx[a] = c[a] + r; }
+        }
         for (int a = 0; a < 3; ++a) {
-            float mn = fminf(fminf(v[a], v[3 + a]), v[6 + a]);
-            float mx = fmaxf(fmaxf(v[a], v[3 + a]), v[6 + a]);
-            prims[i].lo[a] = mn; prims[i].hi[a] = mx;
-            prims[i].c[a] = 0.5f * (mn + mx);
-            maxabs = fmaxf(maxabs, fmaxf(fabsf(mn), fabsf(mx)));
+            prims[i].lo[a] = mn[a]; prims[i].hi[a] = mx[a];
+            prims[i].c[a] = 0.5f * (mn[a] + mx[a]);
+            maxabs = fmaxf(maxabs, fmaxf(fabsf(mn[a]), fabsf(mx[a])));
         }
         prims[i].id = i;
     }
     float pad = maxabs * (1.0f / 65536.0f) + 1e-30f;
-    sc->nodes = (po_node *)malloc(sizeof(po_node) * (size_t)(2 * ntris));
+    sc->nodes = (po_node *)xmalloc(sizeof(po_node) * (size_t)(2 * sc->nprim));
     sc->nnodes = 0;
-    build_rec(sc, prims, 0, ntris, pad);
-    for (int i = 0; i < ntris; ++i) {
-        int id = prims[i].id;
-        po_tri_setup(verts + 9 * (size_t)id, &sc->tris[i]);
-        sc->orig[i] = id;
-        sc->mat[i] = tri_mat[id];
-    }
+    build_rec(sc, prims, 0, sc->nprim, pad);
+    for (int i = 0; i < sc->nprim; ++i) sc->ref[i] = prims[i].id;
     free(prims);
+    return sc;
+}
+
+po_scene *po_scene_create(const float *verts, const int *tri_mat, int ntris, const float *albedo, int nmat,
+                          const po_camera *cam, int accel) {
+    if (nmat < 0) nmat = 0;
+    po_material *mats = (po_material *)xmalloc(sizeof(po_material) * (size_t)nmat);
+    for (int m = 0; m < nmat; ++m) {
+        mats[m].kind = PO_LAMBERTIAN;
+        mats[m].albedo[0] = albedo[3 * m];
+        mats[m].albedo[1] = albedo[3 * m + 1];
+        mats[m].albedo[2] = albedo[3 * m + 2];
+        mats[m].fuzz = 0.0f;
+        mats[m].ir = 1.0f;
+    }
+    po_scene *sc = po_scene_create2(verts, tri_mat, ntris, NULL, NULL, 0, mats, nmat, cam, accel);
+    free(mats);
     return sc;
 }
 
 void po_scene_destroy(po_scene *sc) {
     if (!sc) return;
-    free(sc->tris); free(sc->orig); free(sc->mat); free(sc->albedo); free(sc->nodes);
+    free(sc->tris); free(sc->sph); free(sc->prim_mat); free(sc->mats); free(sc->nodes); free(sc->ref);
     free(sc);
+}
+
+/* Sphere::hit (RayTracer.h:289-314) in the contract's FP32 form: the smaller root if it is
+ * >= tmin, else the larger one (the t_max test of :302-305 is the caller's (t, id) ordering).
+ * The roots of the reference's quadratic are computed in the precision-robust form (Haines et
+ * al., Ray Tracing Gems ch. 7): disc = a (r^2 - |l|^2) with l the centre-to-line vector, and
+ * q = -(hb + sign(hb) sqrt(disc)), roots q/a and c/q.  The reference's literal
+ * hb^2 - a c cancels catastrophically in FP32 when the origin is far from the sphere (t off
+ * by ~1e-3, hit points inside the sphere, paths trapped by self-intersection); in FP64 it
+ * does not, and this form reproduces its roots. */
+int po_sphere_t(const float c[3], float r2, const float o[3], const float d[3], float tmin, float *t) {
+    po_v3 D = ld3(d), oc = vsub(ld3(o), ld3(c));
+    float a = fdot(D, D);
+    float hb = fdot(oc, D);
+    float k = hb / a;
+    po_v3 l = v3(fmaf(-k, D.x, oc.x), fmaf(-k, D.y, oc.y), fmaf(-k, D.z, oc.z));
+    float disc = a * (r2 - fdot(l, l));
+    if (disc < 0.0f) return 0;
+    float sq = sqrtf(disc);
+    float q = hb >= 0.0f ? -(hb + sq) : sq - hb;
+    float cc = fdot(oc, oc) - r2;
+    float t0 = q / a, t1 = cc / q;
+    float tn = fminf(t0, t1), tf = fmaxf(t0, t1);
+    float root = tn;
+    if (!(root >= tmin)) {
+        root = tf;
+        if (!(root >= tmin)) return 0;
+    }
+    *t = root;
+    return 1;
+}
+
+static int prim_hit(const po_scene *sc, int id, const float o[3], const float d[3], float tmin, float *t) {
+    if (id < sc->ntris) return po_tri_hit(&sc->tris[id], o, d, tmin, t);
+    const po_sph *q = &sc->sph[id - sc->ntris];
+    float c[3] = {q->c.x, q->c.y, q->c.z};
+    return po_sphere_t(c, q->r2, o, d, tmin, t);
 }
 
 /* Conservative slab test against a padded box. */
@@ -564,15 +641,21 @@ static inline int box_hit(const po_node *nd, po_v3 o, po_v3 inv, float tmin, flo
     return tn <= tf * 1.0000005f;
 }
 
+/* Closest hit = lexicographic minimum of (t, primitive id) over all primitives with t >= tmin. */
 static int scene_closest(const po_scene *sc, po_v3 o, po_v3 d, float tmin, float *t_out) {
-    if (!sc->accel) {
-        float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
-        return po_closest_hit(sc->tris, sc->orig, sc->ntris, oo, dd, tmin, t_out);
-    }
     float oo[3] = {o.x, o.y, o.z}, dd[3] = {d.x, d.y, d.z};
-    po_v3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     float best = INFINITY;
-    int best_i = -1, best_id = 0x7fffffff;
+    int best_id = -1, best_key = 0x7fffffff; /* the kernels' initial (bestT, bestO) */
+    if (!sc->accel) {
+        for (int id = 0; id < sc->nprim; ++id) {
+            float t;
+            if (!prim_hit(sc, id, oo, dd, tmin, &t)) continue;
+            if (t < best || (t == best && id < best_key)) { best = t; best_id = best_key = id; }
+        }
+        *t_out = best;
+        return best_id;
+    }
+    po_v3 inv = v3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
     int stack[128];
     int sp = 0;
     stack[sp++] = 0;
@@ -581,10 +664,10 @@ static int scene_closest(const po_scene *sc, po_v3 o, po_v3 d, float tmin, float
         if (!box_hit(nd, o, inv, tmin, best)) continue;
         if (nd->right < 0) {
             for (int i = nd->left; i < nd->left - nd->right; ++i) {
+                int id = sc->ref[i];
                 float t;
-                if (!po_tri_hit(&sc->tris[i], oo, dd, tmin, &t)) continue;
-                int id = sc->orig[i];
-                if (t < best || (t == best && id < best_id)) { best = t; best_i = i; best_id = id; }
+                if (!prim_hit(sc, id, oo, dd, tmin, &t)) continue;
+                if (t < best || (t == best && id < best_key)) { best = t; best_id = best_key = id; }
             }
         } else {
             stack[sp++] = nd->right;
@@ -592,7 +675,84 @@ static int scene_closest(const po_scene *sc, po_v3 o, po_v3 d, float tmin, float
         }
     }
     *t_out = best;
-    return best_i;
+    return best_id;
+}
+
+static inline po_v3 vneg(po_v3 a) { return v3(-a.x, -a.y, -a.z); }
+
+/* reflect — RayTracer.h:174-176: v - (2*dot(v,n))*n. */
+static inline po_v3 reflect3(po_v3 v, po_v3 n) {
+    float k = 2.0f * fdot(v, n);
+    return v3(v.x - k * n.x, v.y - k * n.y, v.z - k * n.z);
+}
+
+/* refract — RayTracer.h:178-183, cos_theta = min(dot(-uv, n), 1). */
+static inline po_v3 refract3(po_v3 uv, po_v3 n, float ratio) {
+    float c = fminf(fdot(vneg(uv), n), 1.0f);
+    po_v3 perp = v3((uv.x + c * n.x) * ratio, (uv.y + c * n.y) * ratio, (uv.z + c * n.z) * ratio);
+    float par = -sqrtf(fabsf(1.0f - fdot(perp, perp)));
+    return v3(perp.x + par * n.x, perp.y + par * n.y, perp.z + par * n.z);
+}
+
+void po_reflect(const float v[3], const float n[3], float out[3]) { st3(out, reflect3(ld3(v), ld3(n))); }
+void po_refract(const float uv[3], const float n[3], float ratio, float out[3]) {
+    st3(out, refract3(ld3(uv), ld3(n), ratio));
+}
+
+/* Scatter at a hit (ray_color :585-590 with the material's scatter, :473-540).  Updates the
+ * ray and the throughput; returns 0 when the material absorbs (Metal below the surface). */
+int po_scatter(const po_scene *sc, int prim, float t, float o[3], float d[3], uint32_t *st, float thr[3]) {
+    po_v3 O = ld3(o), D = ld3(d);
+    po_v3 p = v3(fmaf(t, D.x, O.x), fmaf(t, D.y, O.y), fmaf(t, D.z, O.z)); /* Ray::at */
+    po_v3 on;
+    if (prim < sc->ntris) {
+        on = sc->tris[prim].n;
+    } else { /* (p - center) / radius, :308 */
+        const po_sph *q = &sc->sph[prim - sc->ntris];
+        on = v3((p.x - q->c.x) / q->r, (p.y - q->c.y) / q->r, (p.z - q->c.z) / q->r);
+    }
+    int front = fdot(D, on) < 0.0f; /* set_face_normal, :215-218 */
+    po_v3 n = front ? on : vneg(on);
+    const po_material *m = &sc->mats[sc->prim_mat[prim]];
+    po_v3 sd;
+    if (m->kind == PO_METAL) { /* Metal::scatter, :496-501 */
+        po_v3 ud = vscale(D, 1.0f / sqrtf(fdot(D, D)));
+        po_v3 refl = reflect3(ud, n);
+        float r[3];
+        po_random_in_unit_sphere(st, r);
+        sd = v3(refl.x + m->fuzz * r[0], refl.y + m->fuzz * r[1], refl.z + m->fuzz * r[2]);
+        if (!(fdot(sd, n) > 0.0f)) return 0;
+        thr[0] *= m->albedo[0]; thr[1] *= m->albedo[1]; thr[2] *= m->albedo[2];
+    } else if (m->kind == PO_DIELECTRIC) { /* Dielectric::scatter, :512-530 */
+        float ratio = front ? (1.0f / m->ir) : m->ir;
+        po_v3 ud = vscale(D, 1.0f / sqrtf(fdot(D, D)));
+        float cos_t = fminf(fdot(vneg(ud), n), 1.0f);
+        float sin_t = sqrtf(1.0f - cos_t * cos_t);
+        int refl = ratio * sin_t > 1.0f;
+        if (!refl) { /* reflectance (Schlick, :533-538) > random_double(), drawn only here (||) */
+            float r0 = (1.0f - ratio) / (1.0f + ratio);
+            r0 = r0 * r0;
+            float x = 1.0f - cos_t, x2 = x * x;
+            float sch = r0 + (1.0f - r0) * (x2 * x2 * x);
+            refl = sch > po_rand01(st);
+        }
+        if (refl) {
+            sd = reflect3(ud, n);
+        } else {
+            sd = refract3(ud, n, ratio);
+        }
+    } else { /* Lambertian::scatter, :477-484 */
+        float r[3];
+        po_random_in_unit_sphere(st, r);
+        po_v3 rv = ld3(r);
+        po_v3 ru = vscale(rv, 1.0f / sqrtf(fdot(rv, rv)));
+        sd = vadd(n, ru);
+        if (fdot(sd, sd) < 1e-8f) sd = n;
+        thr[0] *= m->albedo[0]; thr[1] *= m->albedo[1]; thr[2] *= m->albedo[2];
+    }
+    st3(o, p);
+    st3(d, sd);
+    return 1;
 }
 
 /* One (pixel, frame) sample: RenderWorker::render's u/v (RayTracerFboItem.cpp:109-110),
@@ -606,12 +766,12 @@ void po_mesh_sample(const po_scene *sc, int width, int height, int x, int y, int
     float t = ((float)y + po_rand01(&st)) * invh;
     float of[3], df[3];
     po_camera_get_ray(&sc->cam, s, t, &st, of, df);
-    po_v3 o = ld3(of), d = ld3(df);
-    po_v3 thr = v3(1.0f, 1.0f, 1.0f);
+    float thr[3] = {1.0f, 1.0f, 1.0f};
     po_v3 L = v3(0.0f, 0.0f, 0.0f);
     int segs = 0;
     for (int depth = 0; depth < max_depth; ++depth) {
         float th;
+        po_v3 o = ld3(of), d = ld3(df);
         int hi = scene_closest(sc, o, d, 0.001f, &th);
         ++segs;
         if (hi < 0) { /* miss: sky gradient, RayTracer.h:593-595 */
@@ -619,23 +779,11 @@ void po_mesh_sample(const po_scene *sc, int width, int height, int x, int y, int
             float a = 0.5f * (uy + 1.0f);
             float b = 1.0f - a;
             po_v3 sky = v3(fmaf(a, 0.5f, b), fmaf(a, 0.7f, b), fmaf(a, 1.0f, b));
-            L = vmul(thr, sky);
+            L = vmul(ld3(thr), sky);
             break;
         }
-        const po_tri *tr = &sc->tris[hi];
-        po_v3 p = v3(fmaf(th, d.x, o.x), fmaf(th, d.y, o.y), fmaf(th, d.z, o.z)); /* Ray::at */
-        po_v3 n = tr->n;
-        if (!(fdot(d, n) < 0.0f)) n = v3(-n.x, -n.y, -n.z); /* set_face_normal */
-        float r[3];
-        po_random_in_unit_sphere(&st, r); /* Lambertian::scatter, RayTracer.h:477-484 */
-        po_v3 rv = ld3(r);
-        po_v3 ru = vscale(rv, 1.0f / sqrtf(fdot(rv, rv)));
-        po_v3 sd = vadd(n, ru);
-        if (fdot(sd, sd) < 1e-8f) sd = n;
-        const float *al = sc->albedo + 3 * (size_t)sc->mat[hi];
-        thr = vmul(thr, ld3(al));
-        o = p;
-        d = sd;
+        if (depth + 1 >= max_depth) break; /* the next ray_color call returns 0 (:582-583) */
+        if (!po_scatter(sc, hi, th, of, df, &st, thr)) break; /* absorbed: 0 (:590) */
     }
     st3(rgb, L);
     if (segs_out) *segs_out = segs;

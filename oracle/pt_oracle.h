@@ -15,13 +15,14 @@
  *
  *  2. "mesh" — the reference CPU path tracer's shading model
  *     (RayTracer.h: Camera :543-576, ray_color :579-596, Lambertian :473-488,
+ *      Metal :490-504, Dielectric :506-540, Sphere::hit :289-314,
  *      random_in_unit_sphere :155-161, random_in_unit_disk :163-169,
- *      set_face_normal :215-218) over triangles, in FP32, driven by the GPU
+ *      set_face_normal :215-218) over triangles and spheres, in FP32, driven by the GPU
  *     kernels' integer-seeded hash RNG (CudaPathTracerKernel.cu:23-35,144) and
  *     accumulated/quantised per CudaPathTracerKernel.cu:157-178.  Triangles are
  *     new capability (the reference has only spheres); the closest hit is
- *     defined BVH-independently as the lexicographic minimum of (t, original
- *     triangle index) over all triangles (see DESIGN.md "Semantic contract").
+ *     defined BVH-independently as the lexicographic minimum of (t, primitive id)
+ *     over all primitives (see DESIGN.md "Semantic contract").
  *
  * Parity pinning: the FP32 helpers are checked against FP64 golden vectors
  * produced by compiling the reference RayTracer.h (oracle/ref_harness.cpp) and
@@ -85,8 +86,25 @@ void po_sphere4_frames(int width, int height, int y0, int y1, int first_frame, i
 
 /* ---- mesh path ---- */
 typedef struct po_scene po_scene;
-/* verts: ntris*9 floats (v0,v1,v2), tri_mat: ntris ints, albedo: nmat*3 floats. accel: 0 = brute force,
- * 1 = oracle-private median-split BVH (results identical by construction; tested). */
+/* Materials (RayTracer.h:473-540): kind PO_LAMBERTIAN uses albedo; PO_METAL albedo + fuzz
+ * (clamped to <= 1 as Metal's constructor does); PO_DIELECTRIC ir. */
+enum { PO_LAMBERTIAN = 0, PO_METAL = 1, PO_DIELECTRIC = 2 };
+typedef struct { int kind; float albedo[3]; float fuzz; float ir; } po_material;
+/* Triangles (verts ntris*9, tri_mat) and spheres (cx, cy, cz, r per sphere, sph_mat); the
+ * primitive id orders ties: triangles 0..ntris-1, then spheres. */
+po_scene *po_scene_create2(const float *verts, const int *tri_mat, int ntris, const float *spheres,
+                           const int *sph_mat, int nsph, const po_material *mats, int nmat, const po_camera *cam,
+                           int accel);
+/* Sphere::hit root selection in the contract's FP32 form (no t_max). */
+int po_sphere_t(const float c[3], float r2, const float o[3], const float d[3], float tmin, float *t);
+/* reflect / refract (RayTracer.h:174-183) in the contract's FP32 form. */
+void po_reflect(const float v[3], const float n[3], float out[3]);
+void po_refract(const float uv[3], const float n[3], float ratio, float out[3]);
+/* Scatter at primitive `prim` hit at t: updates o/d/thr; 0 = absorbed. */
+int po_scatter(const po_scene *sc, int prim, float t, float o[3], float d[3], uint32_t *state, float thr[3]);
+/* Lambertian-only triangle scene: verts: ntris*9 floats (v0,v1,v2), tri_mat: ntris ints, albedo: nmat*3
+ * floats. accel: 0 = brute force, 1 = oracle-private median-split BVH (results identical by
+ * construction; tested). */
 po_scene *po_scene_create(const float *verts, const int *tri_mat, int ntris, const float *albedo, int nmat,
                           const po_camera *cam, int accel);
 void po_scene_destroy(po_scene *sc);

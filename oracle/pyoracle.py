@@ -68,6 +68,10 @@ def lib() -> ctypes.CDLL:
     sig("po_closest_hit", i, ctypes.POINTER(PoTri), pi, i, pf, pf, f, pf)
     sig("po_sphere4_frames", None, i, i, i, i, i, i, i, pf, pu32, i)
     sig("po_scene_create", ctypes.c_void_p, pf, pi, i, pf, i, ctypes.POINTER(PoCamera), i)
+    sig("po_scene_create2", ctypes.c_void_p, pf, pi, i, pf, pi, i, ctypes.c_void_p, i, ctypes.POINTER(PoCamera), i)
+    sig("po_sphere_t", i, pf, f, pf, pf, f, pf)
+    sig("po_reflect", None, pf, pf, pf)
+    sig("po_refract", None, pf, pf, f, pf)
     sig("po_scene_destroy", None, ctypes.c_void_p)
     sig("po_mesh_frames", None, ctypes.c_void_p, i, i, i, i, i, i, i, pf, pu32, pu64, i)
     sig("po_mesh_sample", None, ctypes.c_void_p, i, i, i, i, i, i, pf, pi)
@@ -116,18 +120,23 @@ def sphere4(width, height, first_frame, count, max_depth, y0=0, y1=None, accum=N
 
 
 class MeshScene:
-    """Oracle-side mesh scene (brute-force closest hit when accel=0, private BVH when 1)."""
+    """Oracle-side scene: triangles, spheres, materials (brute-force closest hit when accel=0,
+    private BVH when 1)."""
 
     def __init__(self, scene, width, height, accel=1, cam: PoCamera = None):
         self.scene = scene
         self.width, self.height = width, height
         self.cam = cam if cam is not None else scene_camera(scene, width, height)
-        self._v = np.ascontiguousarray(scene.verts, np.float32)
+        self._v = np.ascontiguousarray(scene.verts, np.float32).reshape(-1, 9)
         self._m = np.ascontiguousarray(scene.tri_mat, np.int32)
-        self._a = np.ascontiguousarray(scene.albedo, np.float32)
-        self.handle = lib().po_scene_create(_p(self._v, ctypes.c_float), _p(self._m, ctypes.c_int),
-                                            int(self._v.shape[0]), _p(self._a, ctypes.c_float),
-                                            int(self._a.shape[0]), ctypes.byref(self.cam), int(accel))
+        self._s = np.ascontiguousarray(getattr(scene, "spheres", np.zeros((0, 4))), np.float32).reshape(-1, 4)
+        self._sm = np.ascontiguousarray(getattr(scene, "sph_mat", np.zeros(0)), np.int32)
+        self._mats = np.ascontiguousarray(scene.materials())  # == po_material layout
+        self.handle = lib().po_scene_create2(_p(self._v, ctypes.c_float), _p(self._m, ctypes.c_int),
+                                             int(self._v.shape[0]), _p(self._s, ctypes.c_float),
+                                             _p(self._sm, ctypes.c_int), int(self._s.shape[0]),
+                                             self._mats.ctypes.data_as(ctypes.c_void_p), int(self._mats.shape[0]),
+                                             ctypes.byref(self.cam), int(accel))
 
     def __del__(self):
         if getattr(self, "handle", None):
@@ -152,6 +161,29 @@ class MeshScene:
         lib().po_mesh_sample(self.handle, self.width, self.height, x, y, frame, max_depth,
                              _p(rgb, ctypes.c_float), ctypes.byref(segs))
         return rgb, segs.value
+
+
+def _f3(v):
+    return (ctypes.c_float * 3)(*[float(x) for x in v])
+
+
+def sphere_t(c, r, o, d, tmin=0.001):
+    """Contract sphere root (po_sphere_t): t or None."""
+    t = ctypes.c_float()
+    ok = lib().po_sphere_t(_f3(c), float(np.float32(r) * np.float32(r)), _f3(o), _f3(d), tmin, ctypes.byref(t))
+    return t.value if ok else None
+
+
+def reflect(v, n):
+    out = (ctypes.c_float * 3)()
+    lib().po_reflect(_f3(v), _f3(n), out)
+    return np.array(out[:], np.float32)
+
+
+def refract(uv, n, ratio):
+    out = (ctypes.c_float * 3)()
+    lib().po_refract(_f3(uv), _f3(n), float(ratio), out)
+    return np.array(out[:], np.float32)
 
 
 def tri_setup(v9) -> PoTri:

@@ -9,6 +9,8 @@
 //              closest hit over triangles) -> tests/golden/*.json
 //   converge — converged radiance image via the reference ray_color (:579-596)
 //              for statistical agreement with the FP32 restatement
+//   random_scene — the reference's random_scene() (spheres, Lambertian/Metal/Dielectric)
+//              dumped as a scene file -> tests/golden/ref_random_scene.scene
 //   bench    — RenderWorker::render (RayTracerFboItem.cpp:46-144) restated without
 //              Qt: hardware_concurrency threads over an atomic tile queue with the
 //              chooseTileSize rule (:793-820); the cpu_baseline of bench.py
@@ -88,27 +90,64 @@ public:
     const Hitable &world;
 };
 
+struct MatDesc {
+    int kind;  // 0 Lambertian, 1 Metal, 2 Dielectric
+    float albedo[3], fuzz, ir;
+};
+
 struct Scene {
     std::vector<float> verts;
     std::vector<int> mat;
-    std::vector<float> albedo;
+    std::vector<float> spheres;  // cx, cy, cz, r
+    std::vector<int> sphMat;
+    std::vector<MatDesc> mats;
     double lookfrom[3], lookat[3], vup[3], vfov, aperture, focus;
 };
 
-// Scene file written by qt-raytracer_amd/hippt/scenes.py (write_scene_file).
+// Scene files written by qt-raytracer_amd/hippt/scenes.py (write_scene_file): v1 'HTPS'
+// (Lambertian triangles), v2 'HTP2' (triangles, spheres, material kinds).
 bool load_scene(const char *path, Scene &s) {
     std::ifstream f(path, std::ios::binary);
     if (!f) return false;
-    int hdr[3];
-    f.read(reinterpret_cast<char *>(hdr), sizeof(hdr));
-    if (hdr[0] != 0x53505448) return false;  // 'HTPS'
-    int nt = hdr[1], nm = hdr[2];
+    int magic = 0;
+    f.read(reinterpret_cast<char *>(&magic), 4);
+    int nt = 0, ns = 0, nm = 0;
+    if (magic == 0x53505448) {
+        int hdr[2];
+        f.read(reinterpret_cast<char *>(hdr), sizeof(hdr));
+        nt = hdr[0];
+        nm = hdr[1];
+    } else if (magic == 0x32505448) {
+        int hdr[3];
+        f.read(reinterpret_cast<char *>(hdr), sizeof(hdr));
+        nt = hdr[0];
+        ns = hdr[1];
+        nm = hdr[2];
+    } else {
+        return false;
+    }
     s.verts.resize(size_t(nt) * 9);
     s.mat.resize(nt);
-    s.albedo.resize(size_t(nm) * 3);
     f.read(reinterpret_cast<char *>(s.verts.data()), s.verts.size() * 4);
     f.read(reinterpret_cast<char *>(s.mat.data()), s.mat.size() * 4);
-    f.read(reinterpret_cast<char *>(s.albedo.data()), s.albedo.size() * 4);
+    s.mats.resize(nm);
+    if (magic == 0x53505448) {
+        std::vector<float> albedo(size_t(nm) * 3);
+        f.read(reinterpret_cast<char *>(albedo.data()), albedo.size() * 4);
+        for (int m = 0; m < nm; ++m) s.mats[m] = MatDesc{0, {albedo[3 * m], albedo[3 * m + 1], albedo[3 * m + 2]}, 0, 1};
+    } else {
+        s.spheres.resize(size_t(ns) * 4);
+        s.sphMat.resize(ns);
+        f.read(reinterpret_cast<char *>(s.spheres.data()), s.spheres.size() * 4);
+        f.read(reinterpret_cast<char *>(s.sphMat.data()), s.sphMat.size() * 4);
+        for (int m = 0; m < nm; ++m) {
+            int kind;
+            float w[5];
+            f.read(reinterpret_cast<char *>(&kind), 4);
+            f.read(reinterpret_cast<char *>(w), sizeof(w));
+            s.mats[m] = MatDesc{kind, {w[0], w[1], w[2]}, w[3], w[4]};
+        }
+    }
     double cam[12];
     f.read(reinterpret_cast<char *>(cam), sizeof(cam));
     for (int i = 0; i < 3; ++i) {
@@ -124,15 +163,66 @@ bool load_scene(const char *path, Scene &s) {
 
 std::vector<std::shared_ptr<Hitable>> make_objects(const Scene &s) {
     std::vector<std::shared_ptr<Material>> mats;
-    for (size_t i = 0; i < s.albedo.size() / 3; ++i)
-        mats.push_back(std::make_shared<Lambertian>(Color(s.albedo[3 * i], s.albedo[3 * i + 1], s.albedo[3 * i + 2])));
+    for (const MatDesc &m : s.mats) {
+        const Color a(m.albedo[0], m.albedo[1], m.albedo[2]);
+        if (m.kind == 1) mats.push_back(std::make_shared<Metal>(a, m.fuzz));
+        else if (m.kind == 2) mats.push_back(std::make_shared<Dielectric>(m.ir));
+        else mats.push_back(std::make_shared<Lambertian>(a));
+    }
     std::vector<std::shared_ptr<Hitable>> objs;
     for (size_t t = 0; t < s.mat.size(); ++t) {
         const float *v = &s.verts[9 * t];
         objs.push_back(std::make_shared<Triangle>(Point3(v[0], v[1], v[2]), Point3(v[3], v[4], v[5]),
                                                   Point3(v[6], v[7], v[8]), mats[s.mat[t]]));
     }
+    for (size_t k = 0; k < s.sphMat.size(); ++k) {
+        const float *q = &s.spheres[4 * k];
+        objs.push_back(std::make_shared<Sphere>(Point3(q[0], q[1], q[2]), q[3], mats[s.sphMat[k]]));
+    }
     return objs;
+}
+
+// The reference's own random_scene() (RayTracer.h:599-643, nondeterministic RNG) dumped as a
+// v2 scene file with RenderWorker::render's camera (RayTracerFboItem.cpp:50-56); coordinates
+// and material parameters are rounded to float, which the file and the GPU path use.
+int cmd_random_scene(const char *out_path) {
+    HitableList world = random_scene();
+    std::vector<float> spheres;
+    std::vector<int> sphMat;
+    std::vector<MatDesc> mats;
+    for (const auto &obj : world.objects) {
+        auto sp = std::dynamic_pointer_cast<Sphere>(obj);
+        if (!sp) return 4;
+        MatDesc m{0, {0, 0, 0}, 0, 1};
+        if (auto l = std::dynamic_pointer_cast<Lambertian>(sp->mat_ptr)) {
+            m = MatDesc{0, {float(l->albedo.x()), float(l->albedo.y()), float(l->albedo.z())}, 0, 1};
+        } else if (auto me = std::dynamic_pointer_cast<Metal>(sp->mat_ptr)) {
+            m = MatDesc{1, {float(me->albedo.x()), float(me->albedo.y()), float(me->albedo.z())}, float(me->fuzz), 1};
+        } else if (auto d = std::dynamic_pointer_cast<Dielectric>(sp->mat_ptr)) {
+            m = MatDesc{2, {1, 1, 1}, 0, float(d->ir)};
+        } else {
+            return 5;
+        }
+        spheres.insert(spheres.end(), {float(sp->center.x()), float(sp->center.y()), float(sp->center.z()),
+                                       float(sp->radius)});
+        sphMat.push_back(int(mats.size()));
+        mats.push_back(m);
+    }
+    FILE *f = std::fopen(out_path, "wb");
+    if (!f) return 2;
+    const int hdr[4] = {0x32505448, 0, int(sphMat.size()), int(mats.size())};
+    std::fwrite(hdr, 4, 4, f);
+    std::fwrite(spheres.data(), 4, spheres.size(), f);
+    std::fwrite(sphMat.data(), 4, sphMat.size(), f);
+    for (const MatDesc &m : mats) {
+        const float w[5] = {m.albedo[0], m.albedo[1], m.albedo[2], m.fuzz, m.ir};
+        std::fwrite(&m.kind, 4, 1, f);
+        std::fwrite(w, 4, 5, f);
+    }
+    const double cam[12] = {13, 2, 3, 0, 0, 0, 0, 1, 0, 20, 0.1, 10};
+    std::fwrite(cam, 8, 12, f);
+    std::fclose(f);
+    return 0;
 }
 
 // Deterministic input generator for golden vectors (not the render RNG).
@@ -405,12 +495,14 @@ int main(int argc, char **argv) {
     if (argc >= 8 && std::strcmp(argv[1], "converge") == 0)
         return cmd_converge(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]), std::atoi(argv[6]),
                             argv[7], argc >= 9 ? std::atoi(argv[8]) : 1);
+    if (argc >= 3 && std::strcmp(argv[1], "random_scene") == 0) return cmd_random_scene(argv[2]);
     if (argc >= 8 && std::strcmp(argv[1], "bench") == 0)
         return cmd_bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]), std::atoi(argv[6]),
                          std::atoi(argv[7]), argc >= 9 ? std::atoi(argv[8]) : 0);
     std::fprintf(stderr,
                  "usage: ref_harness golden OUT.json [SCENE]\n"
                  "       ref_harness converge SCENE W H SPP DEPTH OUT.f32 [THREADS]\n"
-                 "       ref_harness bench SCENE W H STRIDE SPP DEPTH [THREADS]\n");
+                 "       ref_harness bench SCENE W H STRIDE SPP DEPTH [THREADS]\n"
+                 "       ref_harness random_scene OUT.scene\n");
     return 1;
 }

@@ -171,27 +171,27 @@ private:
 
 }  // namespace
 
-bool build_bvh(const float *verts, int numTris, float extentHint, Bvh &out, std::string &err) {
-    if (numTris <= 0) {
+bool build_bvh_boxes(const float *boxes, int numPrims, float extentHint, Bvh &out, std::string &err) {
+    if (numPrims <= 0) {
         // RayTracer.h:398-400: a BVH over an empty range is an error.
-        err = "BVH requires at least one triangle";
+        err = "BVH requires at least one primitive";
         return false;
     }
-    if (numTris >= (1 << 27)) {
-        err = "too many triangles for the 27-bit leaf index";
+    if (numPrims >= (1 << 27)) {
+        err = "too many primitives for the 27-bit leaf index";
         return false;
     }
-    std::vector<Prim> prims(static_cast<size_t>(numTris));
+    std::vector<Prim> prims(static_cast<size_t>(numPrims));
     float maxabs = std::fabs(extentHint);
-    for (int i = 0; i < numTris; ++i) {
-        const float *v = verts + 9 * size_t(i);
+    for (int i = 0; i < numPrims; ++i) {
+        const float *bx = boxes + 6 * size_t(i);
         Prim &p = prims[size_t(i)];
         for (int a = 0; a < 3; ++a) {
-            p.lo[a] = std::min(v[a], std::min(v[3 + a], v[6 + a]));
-            p.hi[a] = std::max(v[a], std::max(v[3 + a], v[6 + a]));
+            p.lo[a] = bx[a];
+            p.hi[a] = bx[3 + a];
             p.c[a] = 0.5f * (p.lo[a] + p.hi[a]);
             if (!std::isfinite(p.lo[a]) || !std::isfinite(p.hi[a])) {
-                err = "non-finite vertex coordinate";
+                err = "non-finite primitive coordinate";
                 return false;
             }
             maxabs = std::max(maxabs, std::max(std::fabs(p.lo[a]), std::fabs(p.hi[a])));
@@ -202,7 +202,7 @@ bool build_bvh(const float *verts, int numTris, float extentHint, Bvh &out, std:
     Builder bld(prims, pad);
     Box rootBox;
     // Node 0 must be interior: reserve it, then build the children.
-    int32_t code = bld.build(0, numTris, 0, rootBox);
+    int32_t code = bld.build(0, numPrims, 0, rootBox);
     if (code < 0) {
         // Whole scene fits one leaf: root holds that leaf and an empty leaf.
         bld.nodes.assign(kNodeWords, 0u);
@@ -212,13 +212,30 @@ bool build_bvh(const float *verts, int numTris, float extentHint, Bvh &out, std:
     out.nodes = std::move(bld.nodes);
     out.levels = bld.levels;
     out.leaves = bld.leaves;
-    out.order.resize(size_t(numTris));
-    for (int i = 0; i < numTris; ++i) out.order[size_t(i)] = prims[size_t(i)].id;
+    out.order.resize(size_t(numPrims));
+    for (int i = 0; i < numPrims; ++i) out.order[size_t(i)] = prims[size_t(i)].id;
     if (out.levels > kStackDepth) {
         err = "BVH deeper than the kernel stack";
         return false;
     }
     return true;
+}
+
+bool build_bvh(const float *verts, int numTris, float extentHint, Bvh &out, std::string &err) {
+    if (numTris <= 0) {
+        err = "BVH requires at least one triangle";
+        return false;
+    }
+    std::vector<float> boxes(size_t(numTris) * 6);
+    for (int i = 0; i < numTris; ++i) {
+        const float *v = verts + 9 * size_t(i);
+        float *bx = &boxes[6 * size_t(i)];
+        for (int a = 0; a < 3; ++a) {
+            bx[a] = std::min(v[a], std::min(v[3 + a], v[6 + a]));
+            bx[3 + a] = std::max(v[a], std::max(v[3 + a], v[6 + a]));
+        }
+    }
+    return build_bvh_boxes(boxes.data(), numTris, extentHint, out, err);
 }
 
 }  // namespace hippt

@@ -20,7 +20,7 @@ constexpr int kNodeWords = 16;  // 64 B: two child boxes + two child codes
 
 struct Bvh {
     std::vector<uint32_t> nodes;  // kNodeWords per interior node; node 0 is the root
-    std::vector<int> order;       // leaf order -> original triangle index
+    std::vector<int> order;       // leaf order -> original primitive index
     int levels = 0;               // interior levels on the deepest path (= max stack use)
     int leaves = 0;
 };
@@ -29,6 +29,9 @@ struct Bvh {
 // (camera position); boxes are padded by max(|coord|, extentHint) * 2^-16 so the
 // kernel's FMA slab test is conservative.
 bool build_bvh(const float *verts, int numTris, float extentHint, Bvh &out, std::string &err);
+// General primitives: boxes = numPrims * 6 floats (lo xyz, hi xyz); `order` maps leaf order
+// to the primitive index.
+bool build_bvh_boxes(const float *boxes, int numPrims, float extentHint, Bvh &out, std::string &err);
 
 inline int32_t leaf_code(int first, int count) { return ~((first << 4) | count); }
 

@@ -50,16 +50,18 @@ struct Ctx {
     unsigned *queue = nullptr;
     unsigned long long *stats = nullptr;
     int sceneVersion = -1;
-    float4 *nodes = nullptr, *tris = nullptr, *shade = nullptr, *albedo = nullptr;
+    float4 *nodes = nullptr, *tris = nullptr, *shade = nullptr, *mats = nullptr;
     // wavefront path-state pool (allocated on first use)
     void *wfPool = nullptr;
     unsigned wfSlots = 0;
     unsigned *wfCtr = nullptr;
     unsigned *wfHost = nullptr;  // pinned: two snapshots of the ray-queue shard counters
     hipEvent_t wfPoll[2] = {nullptr, nullptr};
-    int wfOccKey = -1, wfBlocksPerCu[2] = {0, 0};
+    long long wfOccKey = -1;  // occupancy cached per (scene version, depth, lds, full)
+    int wfBlocksPerCu[2] = {0, 0};
     int cus = 0;
-    int occDepth = -1, meshBlocksPerCu[2] = {0, 0};  // occupancy cached per stack depth
+    long long occKey = -1;  // occupancy cached per (scene version, depth, lds, full)
+    int meshBlocksPerCu[2] = {0, 0};
     std::vector<EventPair> pool;                         // reusable events
     std::vector<std::pair<int, EventPair>> pending;      // (0 trace / 1 combine, events)
     size_t poolUsed = 0;
@@ -68,8 +70,9 @@ struct Ctx {
 struct SceneHost {
     int kind = HIPPT_SCENE_SPHERE4;
     int version = 0;
-    std::vector<float4> nodes, tris, shade, albedo;
-    int numTris = 0, numNodes = 0, levels = 0;
+    std::vector<float4> nodes, tris, shade, mats;  // device layouts (hippt_device.h MeshParams)
+    int numTris = 0, numNodes = 0, levels = 0;  // numTris: primitive records (triangles + spheres)
+    bool full = false;                          // spheres or non-Lambertian materials
     double lookfrom[3] = {0, 0, 0}, lookat[3] = {0, 0, -1}, vup[3] = {0, 1, 0};
     double vfov = 90, aperture = 0, focus = 1;
     bool rawCamera = false;
@@ -178,8 +181,8 @@ void free_scene_buffers(Ctx &c) {
     (void)hipFree(c.nodes);
     (void)hipFree(c.tris);
     (void)hipFree(c.shade);
-    (void)hipFree(c.albedo);
-    c.nodes = c.tris = c.shade = c.albedo = nullptr;
+    (void)hipFree(c.mats);
+    c.nodes = c.tris = c.shade = c.mats = nullptr;
     c.sceneVersion = -1;
 }
 
@@ -236,7 +239,7 @@ bool ensure_scene(Ctx &c, const char **err) {
         return true;
     };
     if (!up(c.nodes, s.scene.nodes) || !up(c.tris, s.scene.tris) || !up(c.shade, s.scene.shade) ||
-        !up(c.albedo, s.scene.albedo))
+        !up(c.mats, s.scene.mats))
         return false;
     c.sceneVersion = s.scene.version;
     return true;
@@ -291,6 +294,10 @@ bool init_locked(int width, int height, const char **err) {
     return false;
 }
 
+long long occupancy_key(int version, int stackDepth, bool lds, bool full) {
+    return ((long long)version << 8) | (stackDepth << 2) | (lds ? 2 : 0) | (full ? 1 : 0);
+}
+
 // Wavefront variant (hippt_wavefront.hip): init + generate, then extend/shade/generate
 // iterations until the ray queue stays empty.  The host reads the queue size with one batch of
 // lag (pinned snapshot + event), so the call returns within ~16 iterations of the end.
@@ -320,11 +327,11 @@ bool run_wavefront(Ctx &c, const hippt::MeshParams &p, bool cnt, const char **er
     W.extQ0 = queues;
     W.extQ1 = queues + size_t(hippt::kWfShards) * shardCap;
     W.genQ = queues + 2 * size_t(hippt::kWfShards) * shardCap;
-    const int occKey = p.stackDepth * 2 + (p.ldsScene ? 1 : 0);
+    const long long occKey = occupancy_key(s.scene.version, p.stackDepth, p.ldsScene != 0, p.full != 0);
     if (c.wfOccKey != occKey) {
         const int ln = p.ldsScene ? p.numNodes : 0, lt = p.ldsScene ? p.numTris : 0;
-        c.wfBlocksPerCu[0] = hippt::wf_extend_blocks_per_cu(false, p.stackDepth, ln, lt);
-        c.wfBlocksPerCu[1] = hippt::wf_extend_blocks_per_cu(true, p.stackDepth, ln, lt);
+        c.wfBlocksPerCu[0] = hippt::wf_extend_blocks_per_cu(false, p.full != 0, p.stackDepth, ln, lt);
+        c.wfBlocksPerCu[1] = hippt::wf_extend_blocks_per_cu(true, p.full != 0, p.stackDepth, ln, lt);
         c.wfOccKey = occKey;
     }
     const int bpc = s.blocksPerCu > 0 ? s.blocksPerCu : c.wfBlocksPerCu[cnt ? 1 : 0];
@@ -418,12 +425,12 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 // small scenes live in LDS (scene bytes beyond the stack under the limit)
                 const bool ldsScene =
                     s.ldsScene && hippt::mesh_lds_bytes(0, numNodes, numTris) <= hippt::mesh_lds_scene_limit();
-                const int occKey = stackDepth * 2 + (ldsScene ? 1 : 0);
-                if (c.occDepth != occKey) {
+                const long long occKey = occupancy_key(s.scene.version, stackDepth, ldsScene, s.scene.full);
+                if (c.occKey != occKey) {
                     const int ln = ldsScene ? numNodes : 0, lt = ldsScene ? numTris : 0;
-                    c.meshBlocksPerCu[0] = hippt::mesh_blocks_per_cu(false, stackDepth, ln, lt);
-                    c.meshBlocksPerCu[1] = hippt::mesh_blocks_per_cu(true, stackDepth, ln, lt);
-                    c.occDepth = occKey;
+                    c.meshBlocksPerCu[0] = hippt::mesh_blocks_per_cu(false, s.scene.full, stackDepth, ln, lt);
+                    c.meshBlocksPerCu[1] = hippt::mesh_blocks_per_cu(true, s.scene.full, stackDepth, ln, lt);
+                    c.occKey = occKey;
                 }
                 int bpc = s.blocksPerCu > 0 ? s.blocksPerCu : c.meshBlocksPerCu[cnt ? 1 : 0];
                 for (int b = 0; b < count; b += fpb) {
@@ -437,7 +444,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.nodes = c.nodes;
                         p.tris = c.tris;
                         p.shade = c.shade;
-                        p.albedo = c.albedo;
+                        p.mats = c.mats;
                         p.scratch = c.scratch;
                         p.queue = c.queue;
                         p.stats = c.stats;
@@ -459,6 +466,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.numNodes = numNodes;
                         p.numTris = numTris;
                         p.ldsScene = ldsScene ? 1 : 0;
+                        p.full = s.scene.full ? 1 : 0;
                         p.waveThreshold = s.waveThreshold;
                         p.chunk = s.chunk;
                         if (s.pathMode == 1) {
@@ -567,28 +575,77 @@ extern "C" bool hipptUseBuiltinScene(int sceneId, const char **err) {
     return true;
 }
 
-extern "C" bool hipptUploadMesh(const float *verts, const int *triMaterial, int numTris, const float *albedo,
-                                int numMaterials, const double lookfrom[3], const double lookat[3],
-                                const double vup[3], double vfovDeg, double aperture, double focusDist,
-                                const char **err) {
+extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int numTris, const float *spheres,
+                                 const int *sphereMaterial, int numSpheres, const hipptMaterial *materials,
+                                 int numMaterials, const double lookfrom[3], const double lookat[3],
+                                 const double vup[3], double vfovDeg, double aperture, double focusDist,
+                                 const char **err) {
     std::lock_guard<std::mutex> g(S().mu);
     State &s = S();
-    if (!verts || !triMaterial || !albedo || !lookfrom || !lookat || !vup) return fail(err, "null scene pointer");
+    if (numTris < 0 || numSpheres < 0) return fail(err, "negative primitive count");
+    if ((numTris > 0 && (!verts || !triMaterial)) || (numSpheres > 0 && (!spheres || !sphereMaterial)) ||
+        !materials || !lookfrom || !lookat || !vup)
+        return fail(err, "null scene pointer");
     if (numMaterials <= 0) return fail(err, "scene needs at least one material");
+    if (numTris + (long long)numSpheres >= (1LL << 27)) return fail(err, "too many primitives");
     for (int i = 0; i < numTris; ++i)
         if (triMaterial[i] < 0 || triMaterial[i] >= numMaterials) return fail(err, "triangle material out of range");
+    for (int j = 0; j < numSpheres; ++j) {
+        if (sphereMaterial[j] < 0 || sphereMaterial[j] >= numMaterials) return fail(err, "sphere material out of range");
+        for (int a = 0; a < 4; ++a)
+            if (!std::isfinite(spheres[4 * j + a])) return fail(err, "non-finite sphere");
+    }
+    bool full = numSpheres > 0;
+    for (int m = 0; m < numMaterials; ++m) {
+        const hipptMaterial &mt = materials[m];
+        if (mt.kind < HIPPT_MAT_LAMBERTIAN || mt.kind > HIPPT_MAT_DIELECTRIC) return fail(err, "unknown material kind");
+        if (!std::isfinite(mt.albedo[0]) || !std::isfinite(mt.albedo[1]) || !std::isfinite(mt.albedo[2]) ||
+            !std::isfinite(mt.fuzz) || !std::isfinite(mt.ir))
+            return fail(err, "non-finite material parameter");
+        full = full || mt.kind != HIPPT_MAT_LAMBERTIAN;
+    }
+    // primitive id p: triangles 0..numTris-1, then spheres (the closest-hit tie order)
+    const int numPrims = numTris + numSpheres;
+    std::vector<float> boxes(size_t(numPrims) * 6);
+    for (int i = 0; i < numTris; ++i) {
+        const float *v = verts + 9 * size_t(i);
+        float *bx = &boxes[6 * size_t(i)];
+        for (int a = 0; a < 3; ++a) {
+            bx[a] = std::min(v[a], std::min(v[3 + a], v[6 + a]));
+            bx[3 + a] = std::max(v[a], std::max(v[3 + a], v[6 + a]));
+        }
+    }
+    for (int j = 0; j < numSpheres; ++j) {
+        const float *q = spheres + 4 * size_t(j);
+        // slack for the FP32 root's error near the box faces (pt_oracle.c po_scene_create2)
+        const float r = std::fabs(q[3]) * (1.0f + 1.0f / 4096.0f);
+        float *bx = &boxes[6 * size_t(numTris + j)];
+        for (int a = 0; a < 3; ++a) {
+            bx[a] = q[a] - r;
+            bx[3 + a] = q[a] + r;
+        }
+    }
     float extent = 0.0f;
     for (int i = 0; i < 3; ++i) extent = std::max(extent, float(std::fabs(lookfrom[i])));
     hippt::Bvh bvh;
     std::string msg;
-    if (!hippt::build_bvh(verts, numTris, extent, bvh, msg)) return fail(err, msg);
+    if (!hippt::build_bvh_boxes(boxes.data(), numPrims, extent, bvh, msg)) return fail(err, msg);
     SceneHost &sc = s.scene;
     sc.nodes.assign(bvh.nodes.size() / 4, float4{});
     std::memcpy(sc.nodes.data(), bvh.nodes.data(), bvh.nodes.size() * sizeof(uint32_t));
-    sc.tris.assign(size_t(numTris) * 3, float4{});
-    sc.shade.assign(size_t(numTris), float4{});
-    for (int k = 0; k < numTris; ++k) {
+    sc.tris.assign(size_t(numPrims) * 3, float4{});
+    sc.shade.assign(size_t(numPrims), float4{});
+    for (int k = 0; k < numPrims; ++k) {
         const int id = bvh.order[size_t(k)];
+        if (id >= numTris) {  // sphere: (center, r) (r^2) (-, id, tag 1); shade (center, mat | flag)
+            const float *q = spheres + 4 * size_t(id - numTris);
+            sc.tris[3 * size_t(k)] = float4{q[0], q[1], q[2], q[3]};
+            sc.tris[3 * size_t(k) + 1] = float4{q[3] * q[3], 0.0f, 0.0f, 0.0f};
+            sc.tris[3 * size_t(k) + 2] = float4{0.0f, as_float(id), as_float(1), 0.0f};
+            sc.shade[size_t(k)] =
+                float4{q[0], q[1], q[2], as_float(sphereMaterial[id - numTris] | hippt::kShadeSphere)};
+            continue;
+        }
         const float *v = verts + 9 * size_t(id);
         // po_tri_setup (oracle) restated: e1 = v1-v0, e2 = v2-v0, n = cross/len
         float e1[3] = {v[3] - v[0], v[4] - v[1], v[5] - v[2]};
@@ -609,12 +666,18 @@ extern "C" bool hipptUploadMesh(const float *verts, const int *triMaterial, int 
         sc.tris[3 * size_t(k) + 2] = float4{e2[2], as_float(id), 0.0f, 0.0f};
         sc.shade[size_t(k)] = float4{n[0], n[1], n[2], as_float(triMaterial[id])};
     }
-    sc.albedo.assign(size_t(numMaterials), float4{});
-    for (int m = 0; m < numMaterials; ++m)
-        sc.albedo[size_t(m)] = float4{albedo[3 * m], albedo[3 * m + 1], albedo[3 * m + 2], 0.0f};
-    sc.numTris = numTris;
+    sc.mats.assign(size_t(numMaterials) * 2, float4{});
+    for (int m = 0; m < numMaterials; ++m) {
+        const hipptMaterial &mt = materials[m];
+        // Metal(a, f): fuzz(f < 1 ? f : 1), RayTracer.h:494
+        const float fuzz = mt.kind == HIPPT_MAT_METAL && !(mt.fuzz < 1.0f) ? 1.0f : mt.fuzz;
+        sc.mats[2 * size_t(m)] = float4{mt.albedo[0], mt.albedo[1], mt.albedo[2], as_float(mt.kind)};
+        sc.mats[2 * size_t(m) + 1] = float4{fuzz, mt.ir, 0.0f, 0.0f};
+    }
+    sc.numTris = numPrims;
     sc.numNodes = int(bvh.nodes.size() / hippt::kNodeWords);
     sc.levels = bvh.levels;
+    sc.full = full;
     for (int i = 0; i < 3; ++i) {
         sc.lookfrom[i] = lookfrom[i];
         sc.lookat[i] = lookat[i];
@@ -627,6 +690,20 @@ extern "C" bool hipptUploadMesh(const float *verts, const int *triMaterial, int 
     sc.kind = HIPPT_SCENE_MESH;
     ++sc.version;
     return true;
+}
+
+extern "C" bool hipptUploadMesh(const float *verts, const int *triMaterial, int numTris, const float *albedo,
+                                int numMaterials, const double lookfrom[3], const double lookat[3],
+                                const double vup[3], double vfovDeg, double aperture, double focusDist,
+                                const char **err) {
+    if (!albedo) return fail(err, "null scene pointer");
+    if (numTris <= 0) return fail(err, "BVH requires at least one triangle");
+    std::vector<hipptMaterial> mats(size_t(std::max(0, numMaterials)));
+    for (int m = 0; m < numMaterials; ++m)
+        mats[size_t(m)] = hipptMaterial{HIPPT_MAT_LAMBERTIAN, {albedo[3 * m], albedo[3 * m + 1], albedo[3 * m + 2]}, 0.0f,
+                                        1.0f};
+    return hipptUploadScene(verts, triMaterial, numTris, nullptr, nullptr, 0, mats.data(), numMaterials, lookfrom,
+                            lookat, vup, vfovDeg, aperture, focusDist, err);
 }
 
 extern "C" bool hipptSetCamera(const hipptCamera *camera, const char **err) {

@@ -27,9 +27,14 @@ struct Sphere4Params {
 // samples of rows [y0, y0+bandRows) and frames [firstFrame, firstFrame+frames).
 struct MeshParams {
     const float4 *nodes;   // 4 float4 per interior node (bvh_builder.h layout)
-    const float4 *tris;    // 3 float4 per triangle: (v0, e1.x) (e1.yz, e2.xy) (e2.z, orig, -, -)
-    const float4 *shade;   // 1 float4 per triangle: unit normal xyz, material index (int bits)
-    const float4 *albedo;  // 1 float4 per material
+    // 3 float4 per primitive, BVH leaf order, tag = third .z (int bits):
+    //   triangle (tag 0): (v0, e1.x) (e1.yz, e2.xy) (e2.z, prim id, 0, -)
+    //   sphere   (tag 1): (center, radius) (radius^2, -, -, -) (-, prim id, 1, -)
+    const float4 *tris;
+    // 1 float4 per primitive: triangle (unit normal, material), sphere (center, material |
+    // kShadeSphere); material index as int bits
+    const float4 *shade;
+    const float4 *mats;    // 2 float4 per material: (albedo rgb, kind) (fuzz, ir, -, -)
     float *scratch;        // 3 planes (R, G, B) of totalItems floats: per-sample radiance
     unsigned *queue;       // global work counter (zeroed before launch)
     unsigned long long *stats;  // [0] segments, [1] pixel samples, [2] node visits, [3] tri tests
@@ -42,6 +47,7 @@ struct MeshParams {
     int stackDepth;        // LDS stack entries per lane (>= BVH interior levels)
     int numNodes, numTris;
     int ldsScene;          // 1: copy nodes/triangles/shading into LDS (small scenes)
+    int full;              // 1: spheres or non-Lambertian materials present (general kernel)
     int waveThreshold;     // shade once fewer than this many lanes still traverse
     unsigned chunk;        // items per queue grab (multiple of 64)
 };
@@ -56,11 +62,15 @@ struct CombineParams {
     int firstFrame, frames;
 };
 
+// Material kinds (RayTracer.h:473-540) and the sphere flag of a shading record.
+enum { kLambertian = 0, kMetal = 1, kDielectric = 2 };
+constexpr int kShadeSphere = 1 << 30;
+
 hipError_t launch_sphere4(const Sphere4Params &p, hipStream_t s);
 hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hipStream_t s);
 hipError_t launch_combine(const CombineParams &p, hipStream_t s);
 // Resident mesh-kernel blocks per CU for a given LDS stack depth and LDS scene size.
-int mesh_blocks_per_cu(bool countTraversal, int stackDepth, int ldsNodes, int ldsTris);
+int mesh_blocks_per_cu(bool countTraversal, bool full, int stackDepth, int ldsNodes, int ldsTris);
 size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris);
 size_t mesh_lds_scene_limit();
 constexpr int kMeshBlock = 256;

@@ -1,6 +1,12 @@
-// hippt_trace.h — device building blocks of the triangle path tracer shared by the wavefront
-// kernels (hippt_wavefront.hip).  Same arithmetic contract as hippt_kernels.hip and
-// oracle/pt_oracle.c: -ffp-contract=off, FMAs only where written, IEEE division/sqrt.
+// hippt_trace.h — device building blocks of the mesh path tracer, shared by the megakernel
+// (hippt_kernels.hip) and the wavefront kernels (hippt_wavefront.hip): RNG, camera ray,
+// BVH traversal round, primitive tests, sky and material scatter.
+//
+// Arithmetic contract (oracle/pt_oracle.c): compiled with -ffp-contract=off; the only fused
+// multiply-adds are the explicit fmaf() calls, placed where the oracle places them, and
+// division/sqrt are IEEE correctly rounded (hipcc default), so every result-defining value is
+// bit-identical to the CPU restatement.  The BVH box test is NOT result-defining (boxes are
+// padded; the closest hit is argmin (t, primitive id)), so it uses the fast reciprocal.
 #pragma once
 
 #include "bvh_builder.h"
@@ -95,6 +101,18 @@ __device__ __forceinline__ void wave_append(bool req, unsigned value, unsigned *
     if (req) queue[base + rank] = value;
 }
 
+// Phase profiling (STATS builds): pc[2k] counts wave-level passes of phase k (by the first
+// active lane), pc[2k+1] lane-level passes; SIMD efficiency = lanes / (64 * waves).  Phases:
+// 0 outer iteration, 1 camera ray, 2 traversal round, 3 interior node loop, 4 leaf loop,
+// 5 primitive test, 6 shading, 7 unit-sphere rejection loop.
+template <bool STATS>
+__device__ __forceinline__ void prof(unsigned *pc, int k) {
+    if (STATS) {
+        ++pc[2 * k + 1];
+        if (__lane_id() == unsigned(__ffsll((unsigned long long)__ballot(1)) - 1)) ++pc[2 * k];
+    }
+}
+
 struct Ray {
     float ox, oy, oz, dx, dy, dz;
     float ix, iy, iz, oix, oiy, oiz;  // box-test reciprocals (fast rcp; not result-defining)
@@ -152,19 +170,12 @@ __device__ __forceinline__ void sky(const Ray &r, float tr, float tg, float tb, 
     L2 = tb * fmaf(al, 1.0f, bl);
 }
 
-// Lambertian scatter at hit (t, shading record sh): ray_color / Lambertian::scatter
-// (RayTracer.h:585-589, :477-484), throughput *= albedo.
-__device__ __forceinline__ void scatter(Ray &r, float t, float4 sh, const float4 *albedo, uint32_t &rng, float &tr,
-                                        float &tg, float &tb) {
-    float nx = sh.x, ny = sh.y, nz = sh.z;
-    const float px = fmaf(t, r.dx, r.ox), py = fmaf(t, r.dy, r.oy), pz = fmaf(t, r.dz, r.oz);
-    if (!(fdot(r.dx, r.dy, r.dz, nx, ny, nz) < 0.0f)) {  // set_face_normal, :215-218
-        nx = -nx;
-        ny = -ny;
-        nz = -nz;
-    }
-    float rx, ry, rz, r2;
-    for (unsigned tries = 1;; ++tries) {  // random_in_unit_sphere, :155-161
+// random_in_unit_sphere (RayTracer.h:155-161; x, y, z drawn in that order).
+template <bool STATS>
+__device__ __forceinline__ float rius(uint32_t &rng, float &rx, float &ry, float &rz, unsigned *pc) {
+    float r2;
+    for (unsigned tries = 1;; ++tries) {
+        prof<STATS>(pc, 7);
         rx = fmaf(2.0f, rand01(rng), -1.0f);
         ry = fmaf(2.0f, rand01(rng), -1.0f);
         rz = fmaf(2.0f, rand01(rng), -1.0f);
@@ -172,23 +183,124 @@ __device__ __forceinline__ void scatter(Ray &r, float t, float4 sh, const float4
         if (r2 < 1.0f) break;
         escape_cycle(rng, tries);
     }
-    const float inv = 1.0f / sqrtf(r2);
-    float sx = nx + rx * inv, sy = ny + ry * inv, sz = nz + rz * inv;
-    if (fdot(sx, sy, sz, sx, sy, sz) < 1e-8f) {
-        sx = nx;
-        sy = ny;
-        sz = nz;
+    return r2;
+}
+
+// Scatter at the closest hit (ray_color :585-590 + the material's scatter, :473-540) of
+// primitive `prim` at t.  The ray becomes the scattered ray and the throughput takes the
+// attenuation; false = absorbed (Metal below the surface), which contributes 0.  FULL=false
+// is the Lambertian-triangle specialisation (no sphere normals, no material dispatch).
+template <bool FULL, bool STATS>
+__device__ __forceinline__ bool scatter(Ray &r, float t, int prim, const float4 *shade, const float4 *prims,
+                                        const float4 *mats, uint32_t &rng, float &tr, float &tg, float &tb,
+                                        unsigned *pc) {
+    const float4 sh = shade[prim];
+    const int mw = __float_as_int(sh.w);
+    const float px = fmaf(t, r.dx, r.ox), py = fmaf(t, r.dy, r.oy), pz = fmaf(t, r.dz, r.oz);  // Ray::at
+    float nx = sh.x, ny = sh.y, nz = sh.z;
+    if (FULL && (mw & kShadeSphere)) {  // (p - center) / radius, :308
+        const float rad = prims[3 * prim].w;
+        nx = (px - sh.x) / rad;
+        ny = (py - sh.y) / rad;
+        nz = (pz - sh.z) / rad;
     }
-    const float4 alb = albedo[__float_as_int(sh.w)];
-    tr *= alb.x;
-    tg *= alb.y;
-    tb *= alb.z;
+    const bool front = fdot(r.dx, r.dy, r.dz, nx, ny, nz) < 0.0f;  // set_face_normal, :215-218
+    if (!front) {
+        nx = -nx;
+        ny = -ny;
+        nz = -nz;
+    }
+    const int m = FULL ? (mw & ~kShadeSphere) : mw;
+    const float4 m0 = mats[2 * m];
+    float sx, sy, sz;
+    const int kind = FULL ? __float_as_int(m0.w) : int(kLambertian);
+    if (kind == kMetal) {  // Metal::scatter, :496-501
+        const float fuzz = mats[2 * m + 1].x;
+        const float il = 1.0f / sqrtf(fdot(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz));
+        const float ux = r.dx * il, uy = r.dy * il, uz = r.dz * il;
+        const float k = 2.0f * fdot(ux, uy, uz, nx, ny, nz);  // reflect, :174-176
+        float qx, qy, qz;
+        rius<STATS>(rng, qx, qy, qz, pc);
+        sx = (ux - k * nx) + fuzz * qx;
+        sy = (uy - k * ny) + fuzz * qy;
+        sz = (uz - k * nz) + fuzz * qz;
+        if (!(fdot(sx, sy, sz, nx, ny, nz) > 0.0f)) return false;
+        tr *= m0.x;
+        tg *= m0.y;
+        tb *= m0.z;
+    } else if (kind == kDielectric) {  // Dielectric::scatter, :512-530 (attenuation 1)
+        const float ir = mats[2 * m + 1].y;
+        const float ratio = front ? (1.0f / ir) : ir;
+        const float il = 1.0f / sqrtf(fdot(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz));
+        const float ux = r.dx * il, uy = r.dy * il, uz = r.dz * il;
+        const float cosT = fminf(fdot(-ux, -uy, -uz, nx, ny, nz), 1.0f);
+        const float sinT = sqrtf(1.0f - cosT * cosT);
+        bool refl = ratio * sinT > 1.0f;
+        if (!refl) {  // Schlick (:533-538) > random_double(), drawn only when refraction is possible
+            float r0 = (1.0f - ratio) / (1.0f + ratio);
+            r0 = r0 * r0;
+            const float x = 1.0f - cosT, x2 = x * x;
+            refl = r0 + (1.0f - r0) * (x2 * x2 * x) > rand01(rng);
+        }
+        if (refl) {
+            const float k = 2.0f * fdot(ux, uy, uz, nx, ny, nz);
+            sx = ux - k * nx;
+            sy = uy - k * ny;
+            sz = uz - k * nz;
+        } else {  // refract, :178-183
+            const float qx = (ux + cosT * nx) * ratio, qy = (uy + cosT * ny) * ratio, qz = (uz + cosT * nz) * ratio;
+            const float par = -sqrtf(fabsf(1.0f - fdot(qx, qy, qz, qx, qy, qz)));
+            sx = qx + par * nx;
+            sy = qy + par * ny;
+            sz = qz + par * nz;
+        }
+    } else {  // Lambertian::scatter, :477-484: n + unit(random_in_unit_sphere), 1e-8 fallback
+        float qx, qy, qz;
+        const float r2 = rius<STATS>(rng, qx, qy, qz, pc);
+        const float inv = 1.0f / sqrtf(r2);  // unit_vector = (1/len)*v, :137-139,151-153
+        sx = nx + qx * inv;
+        sy = ny + qy * inv;
+        sz = nz + qz * inv;
+        if (fdot(sx, sy, sz, sx, sy, sz) < 1e-8f) {
+            sx = nx;
+            sy = ny;
+            sz = nz;
+        }
+        tr *= m0.x;
+        tg *= m0.y;
+        tb *= m0.z;
+    }
     r.ox = px;
     r.oy = py;
     r.oz = pz;
     r.dx = sx;
     r.dy = sy;
     r.dz = sz;
+    return true;
+}
+
+// Sphere::hit (RayTracer.h:289-314) root selection in the contract's FP32 form
+// (pt_oracle.c po_sphere_t: precision-robust roots of the reference's quadratic): the
+// smaller root if >= tmin, else the larger.
+__device__ __forceinline__ bool sphere_t(float4 A, float r2, const Ray &r, float tmin, float &t) {
+    const float ocx = r.ox - A.x, ocy = r.oy - A.y, ocz = r.oz - A.z;
+    const float a = fdot(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz);
+    const float hb = fdot(ocx, ocy, ocz, r.dx, r.dy, r.dz);
+    const float k = hb / a;
+    const float lx = fmaf(-k, r.dx, ocx), ly = fmaf(-k, r.dy, ocy), lz = fmaf(-k, r.dz, ocz);
+    const float disc = a * (r2 - fdot(lx, ly, lz, lx, ly, lz));
+    if (disc < 0.0f) return false;
+    const float sq = sqrtf(disc);
+    const float q = hb >= 0.0f ? -(hb + sq) : sq - hb;
+    const float cc = fdot(ocx, ocy, ocz, ocx, ocy, ocz) - r2;
+    const float t0 = q / a, t1 = cc / q;
+    float root = fminf(t0, t1);
+    if (!(root >= tmin)) {
+        root = fmaxf(t0, t1);
+        if (!(root >= tmin)) return false;
+    }
+    t = root;
+    return true;
 }
 
 struct Trav {
@@ -210,16 +322,21 @@ __device__ __forceinline__ void begin(Trav &T) {
 
 // One speculative while-while round (Aila & Laine 2009) over the BVH: interior loop until
 // every lane still in it holds a postponed leaf, then the leaf loop.  `my` = this lane's
-// LDS stack column (entry k at my[k*kMeshBlock]).  Closest hit = min (t, original index).
-template <int NODE_F4>
+// LDS stack column (entry k at my[k*kMeshBlock]).  Closest hit = min (t, primitive id).
+// Interior nodes: the far child is written to the slot above the top unconditionally (one
+// spare slot per lane) and kept only when both children are hit; the top is read
+// unconditionally and used only when neither is (branch-free child selection).
+template <int NODE_F4, bool STATS, bool FULL>
 __device__ __forceinline__ void traverse_round(Trav &T, const Ray &r, int *my, const float4 *nodes,
-                                               const float4 *tris, unsigned &nvis, unsigned &ntest) {
+                                               const float4 *tris, unsigned long long &nvis,
+                                               unsigned long long &ntest, unsigned *pc) {
     const float tmin = 0.001f;
     while (T.cur >= 0) {
-        const float4 *nd = nodes + __umul24(unsigned(T.cur), unsigned(NODE_F4));
+        prof<STATS>(pc, 3);
+        const float4 *nd = nodes + __umul24(unsigned(T.cur), unsigned(NODE_F4));  // full-rate 24-bit mul
         const float4 a = nd[0], b = nd[1], c = nd[2];
         const int4 e = *reinterpret_cast<const int4 *>(nd + 3);
-        ++nvis;
+        if (STATS) ++nvis;
         const float l0x = fmaf(a.x, r.ix, -r.oix), h0x = fmaf(a.w, r.ix, -r.oix);
         const float l0y = fmaf(a.y, r.iy, -r.oiy), h0y = fmaf(b.x, r.iy, -r.oiy);
         const float l0z = fmaf(a.z, r.iz, -r.oiz), h0z = fmaf(b.y, r.iz, -r.oiz);
@@ -231,15 +348,17 @@ __device__ __forceinline__ void traverse_round(Trav &T, const Ray &r, int *my, c
         const float n1 = fmaxf(fmaxf(fminf(l1x, h1x), fminf(l1y, h1y)), fmaxf(fminf(l1z, h1z), tmin));
         const float f1 = fminf(fminf(fmaxf(l1x, h1x), fmaxf(l1y, h1y)), fminf(fmaxf(l1z, h1z), T.bestT));
         const bool hit0 = n0 <= f0, hit1 = n1 <= f1;
-        const bool take0 = hit0 & (!hit1 | (n0 <= n1));
+        const bool take0 = hit0 & (!hit1 | (n0 <= n1));  // bitwise: no exec-mask branches
         const int nearC = take0 ? e.x : e.y;
         const int farC = take0 ? e.y : e.x;
         my[T.sp] = farC;
         const int top = my[max(T.sp - kMeshBlock, 0)];
+        // (logical, not bitwise, operators here: measured 4.5% faster on gfx950)
         const bool none = !(hit0 || hit1);
         T.sp += (hit0 && hit1) ? kMeshBlock : 0;
         T.cur = none ? (T.sp > 0 ? top : kDone) : nearC;
         T.sp -= (none && T.sp > 0) ? kMeshBlock : 0;
+        // postpone the first leaf reached and keep descending
         if (T.cur < 0 && T.cur != kDone && T.leaf == 0) {
             T.leaf = T.cur;
             T.cur = T.sp > 0 ? my[T.sp -= kMeshBlock] : kDone;
@@ -247,12 +366,25 @@ __device__ __forceinline__ void traverse_round(Trav &T, const Ray &r, int *my, c
         if (!__any(T.leaf == 0)) break;
     }
     while (T.leaf != 0) {
+        prof<STATS>(pc, 4);
         const int code = ~T.leaf;
         const int first = code >> 4, last = first + (code & 15);
         for (int i = first; i < last; ++i) {
             const float4 *tp = tris + 3 * i;
             const float4 A = tp[0], B = tp[1], Cc = tp[2];
-            ++ntest;
+            prof<STATS>(pc, 5);
+            if (STATS) ++ntest;
+            if (FULL && __float_as_int(Cc.z) != 0) {
+                float tt;
+                const int orig = __float_as_int(Cc.y);
+                if (sphere_t(A, B.x, r, tmin, tt) && (tt < T.bestT || (tt == T.bestT && orig < T.bestO))) {
+                    T.bestT = tt;
+                    T.bestI = i;
+                    T.bestO = orig;
+                }
+                continue;
+            }
+            // Möller–Trumbore, division-free edge tests (pt_oracle.c po_tri_hit)
             const float e1x = A.w, e1y = B.x, e1z = B.y;
             const float e2x = B.z, e2y = B.w, e2z = Cc.x;
             const float pvx = fmaf(r.dy, e2z, -(r.dz * e2y));
@@ -277,6 +409,7 @@ __device__ __forceinline__ void traverse_round(Trav &T, const Ray &r, int *my, c
                 }
             }
         }
+        // a leaf that was next in line is processed in the same loop
         T.leaf = 0;
         if (T.cur < 0 && T.cur != kDone) {
             T.leaf = T.cur;

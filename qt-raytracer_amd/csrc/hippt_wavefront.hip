@@ -5,7 +5,7 @@
 //   wf_extend    persistent grid; lanes pull ray-queue entries (wave-pooled counter), traverse
 //                the BVH (the megakernel's speculative while-while round, threshold refill)
 //                and write (t, triangle) per slot;
-//   wf_shade     one lane per queued slot: sky on a miss, depth cut-off, or Lambertian scatter;
+//   wf_shade     one lane per queued slot: sky on a miss, depth cut-off, or material scatter;
 //                scattered slots go to the next ray queue, finished samples write their radiance
 //                to the sample scratch and go to the regenerate queue;
 //   wf_generate  one lane per regenerate-queue entry: work item = base + queue position (no
@@ -97,7 +97,7 @@ __global__ void wf_init(WfParams W) {
     if (i == 0) W.ctr[ctr_word(kCtrWork)] = 0;
 }
 
-template <bool STATS, bool LDS_SCENE>
+template <bool STATS, bool LDS_SCENE, bool FULL>
 __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
     extern __shared__ int stk[];
     int *const my = stk + threadIdx.x;
@@ -141,7 +141,8 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
     T.bestT = INFINITY;
     T.bestI = -1;
     T.bestO = 0x7fffffff;
-    unsigned nvis = 0, ntest = 0;
+    unsigned long long nvis = 0, ntest = 0;
+    unsigned pc[16];  // phase profile slots (unused here)
     for (;;) {
         while (left && __ballot(need)) {
             const unsigned qi =
@@ -163,7 +164,7 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
         need = false;
         if (!__any(T.cur != kDone)) break;
         do {
-            traverse_round<LDS_SCENE ? 5 : 4>(T, r, my, nodes, tris, nvis, ntest);
+            traverse_round<LDS_SCENE ? 5 : 4, false, FULL>(T, r, my, nodes, tris, nvis, ntest, pc);
         } while (__popcll(__ballot(T.cur != kDone)) > unsigned(P.waveThreshold));
         if (slot != kNone && T.cur == kDone) {
             *reinterpret_cast<float2 *>(W.st + 4 * size_t(slot) + 3) = make_float2(T.bestT, __int_as_float(T.bestI));
@@ -183,6 +184,7 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
 // Shade and generate keep every shard an independent pipeline: block b works on shard
 // b % kWfShards and appends back to the same shard, so a shard never holds more than its
 // initial ceil(slots / kWfShards) entries.
+template <bool FULL>
 __global__ __launch_bounds__(kWfBlock) void wf_shade(WfParams W, int cur) {
     __shared__ unsigned lds[kWfBlock / 64 + 1];
     const MeshParams &P = W.mp;
@@ -215,10 +217,11 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(WfParams W, int cur) {
             finished = true;
         } else if (++q.depth >= P.maxDepth) {
             finished = true;
-        } else {
-            scatter(q.r, h.x, P.shade[tri], P.albedo, q.rng, q.tr, q.tg, q.tb);
+        } else if (scatter<FULL, false>(q.r, h.x, tri, P.shade, P.tris, P.mats, q.rng, q.tr, q.tg, q.tb, nullptr)) {
             store_slot(W, slot, q);
             again = true;
+        } else {
+            finished = true;  // absorbed: contributes 0
         }
         if (finished) {
             P.scratch[q.item] = L0;
@@ -265,9 +268,13 @@ __global__ __launch_bounds__(kWfBlock) void wf_generate(WfParams W, int nxt, int
 }
 
 using ExtFn = void (*)(WfParams, int);
-ExtFn ext_fn(bool count, bool lds) {
-    if (count) return lds ? wf_extend<true, true> : wf_extend<true, false>;
-    return lds ? wf_extend<false, true> : wf_extend<false, false>;
+ExtFn ext_fn(bool count, bool lds, bool full) {
+    if (full) {
+        if (count) return lds ? wf_extend<true, true, true> : wf_extend<true, false, true>;
+        return lds ? wf_extend<false, true, true> : wf_extend<false, false, true>;
+    }
+    if (count) return lds ? wf_extend<true, true, false> : wf_extend<true, false, false>;
+    return lds ? wf_extend<false, true, false> : wf_extend<false, false, false>;
 }
 
 }  // namespace
@@ -298,19 +305,19 @@ hipError_t wf_launch_extend(const WfParams &W, int cur, int blocks, bool countTr
     const MeshParams &P = W.mp;
     const bool lds = P.ldsScene != 0;
     const size_t bytes = mesh_lds_bytes(P.stackDepth, lds ? P.numNodes : 0, lds ? P.numTris : 0);
-    hipLaunchKernelGGL(ext_fn(countTraversal, lds), dim3(blocks), dim3(kMeshBlock), bytes, s, W, cur);
+    hipLaunchKernelGGL(ext_fn(countTraversal, lds, P.full != 0), dim3(blocks), dim3(kMeshBlock), bytes, s, W, cur);
     return hipGetLastError();
 }
 
 hipError_t wf_launch_shade(const WfParams &W, int cur, hipStream_t s) {
-    hipLaunchKernelGGL(wf_shade, dim3(shard_grid(W)), dim3(kWfBlock), 0, s, W, cur);
+    hipLaunchKernelGGL(W.mp.full ? wf_shade<true> : wf_shade<false>, dim3(shard_grid(W)), dim3(kWfBlock), 0, s, W, cur);
     return hipGetLastError();
 }
 
-int wf_extend_blocks_per_cu(bool countTraversal, int stackDepth, int ldsNodes, int ldsTris) {
+int wf_extend_blocks_per_cu(bool countTraversal, bool full, int stackDepth, int ldsNodes, int ldsTris) {
     int n = 0;
     const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ext_fn(countTraversal, ldsNodes > 0), kMeshBlock, bytes) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ext_fn(countTraversal, ldsNodes > 0, full), kMeshBlock, bytes) !=
             hipSuccess ||
         n <= 0)
         n = 1;

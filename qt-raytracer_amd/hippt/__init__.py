@@ -39,7 +39,7 @@ OPT_WAVEFRONT_SLOTS = 9
 EXPORTS = (
     "cudaPathTracerInit", "cudaPathTracerRender", "cudaPathTracerShutdown",
     "hipPathTracerInit", "hipPathTracerRender", "hipPathTracerShutdown",
-    "hipptBuildCamera", "hipptUseBuiltinScene", "hipptUploadMesh", "hipptSetCamera",
+    "hipptBuildCamera", "hipptUseBuiltinScene", "hipptUploadMesh", "hipptUploadScene", "hipptSetCamera",
     "hipptDeviceCount", "hipptSetDevices", "hipptSetRowRange",
     "hipptRenderFrames", "hipptRenderFramesAsync", "hipptSynchronize", "hipptReadback",
     "hipptResetAccumulation", "hipptGetStats", "hipptResetStats", "hipptGetCounters", "hipptSetOption",
@@ -110,6 +110,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     sig("hipptUseBuiltinScene", c_bool, c_int, pp_char)
     sig("hipptUploadMesh", c_bool, p_float, p_int, c_int, p_float, c_int, p_double, p_double, p_double,
         c_double, c_double, c_double, pp_char)
+    sig("hipptUploadScene", c_bool, p_float, p_int, c_int, p_float, p_int, c_int, ctypes.c_void_p, c_int, p_double,
+        p_double, p_double, c_double, c_double, c_double, pp_char)
     sig("hipptSetCamera", c_bool, ctypes.POINTER(Camera), pp_char)
     sig("hipptDeviceCount", c_int)
     sig("hipptSetDevices", c_bool, p_int, c_int, pp_char)
@@ -280,7 +282,26 @@ class PathTracer:
         if not self._lib.hipptUseBuiltinScene(int(scene_id), ctypes.byref(e)):
             raise HipptError(_err(e, "bad scene"))
 
+    def uploadScene(self, scene) -> None:  # noqa: N802
+        """hipptUploadScene: triangles + spheres + materials (hippt.scenes.Scene)."""
+        v = np.ascontiguousarray(scene.verts, dtype=np.float32).reshape(-1, 9)
+        m = np.ascontiguousarray(scene.tri_mat, dtype=np.int32)
+        sp = np.ascontiguousarray(scene.spheres, dtype=np.float32).reshape(-1, 4)
+        sm = np.ascontiguousarray(scene.sph_mat, dtype=np.int32)
+        mats = np.ascontiguousarray(scene.materials())
+        e = ctypes.c_char_p()
+        ok = self._lib.hipptUploadScene(_ptr(v, ctypes.c_float), _ptr(m, ctypes.c_int), int(v.shape[0]),
+                                        _ptr(sp, ctypes.c_float), _ptr(sm, ctypes.c_int), int(sp.shape[0]),
+                                        mats.ctypes.data_as(ctypes.c_void_p), int(mats.shape[0]),
+                                        _d3(scene.lookfrom), _d3(scene.lookat), _d3(scene.vup), float(scene.vfov),
+                                        float(scene.aperture), float(scene.focus), ctypes.byref(e))
+        if not ok:
+            raise HipptError(_err(e, "scene upload failed"))
+
     def uploadMesh(self, scene) -> None:  # noqa: N802
+        """hipptUploadMesh for Lambertian triangle scenes; other scenes go through uploadScene."""
+        if not getattr(scene, "lambertian_triangles", True):
+            return self.uploadScene(scene)
         v = np.ascontiguousarray(scene.verts, dtype=np.float32).reshape(-1, 9)
         m = np.ascontiguousarray(scene.tri_mat, dtype=np.int32)
         a = np.ascontiguousarray(scene.albedo, dtype=np.float32).reshape(-1, 3)

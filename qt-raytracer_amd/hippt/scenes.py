@@ -13,10 +13,23 @@ CudaPathTracerKernel.cu:113-116), so the benchmark scenes are defined here:
 
 Camera (both): lookfrom (278, 278, -800) -> lookat (278, 278, 0), vup +y, vfov 40,
 aperture 0, focus distance 10 (RayTracerFboItem.cpp:49-56 uses 10).
+
+Scenes with spheres and the reference's other materials (RayTracer.h:490-540):
+
+* ``random_scene`` — the recipe of RayTracer.h ``random_scene`` (:599-643: ground sphere,
+  22 x 22 jittered small spheres, 80% Lambertian / 15% Metal / 5% Dielectric, three big
+  spheres) drawn from a seeded numpy RNG (the reference's own RNG is nondeterministic,
+  RayTracer.h:25-55), with RenderWorker::render's camera (RayTracerFboItem.cpp:50-56).
+  ``load_scene_file(tests/golden/ref_random_scene.scene)`` is one scene the reference
+  itself generated.
+* ``cornell_mixed`` — the Cornell walls and the short box, a metal tall box, a glass
+  sphere on the short box and a fuzzy metal sphere: triangles and spheres, all three
+  materials.
 """
 from __future__ import annotations
 
 import dataclasses
+import os
 import struct
 
 import numpy as np
@@ -25,7 +38,12 @@ WHITE = (0.73, 0.73, 0.73)
 GREEN = (0.12, 0.45, 0.15)
 RED = (0.65, 0.05, 0.05)
 
-SCENE_MAGIC = 0x53505448
+SCENE_MAGIC = 0x53505448      # v1: Lambertian triangles
+SCENE_MAGIC_V2 = 0x32505448   # v2: triangles, spheres, material kinds
+
+MAT_LAMBERTIAN, MAT_METAL, MAT_DIELECTRIC = 0, 1, 2
+# == hipptMaterial (include/hippt.h) == po_material (oracle/pt_oracle.h)
+MATERIAL_DTYPE = np.dtype([("kind", "<i4"), ("albedo", "<f4", (3,)), ("fuzz", "<f4"), ("ir", "<f4")])
 
 
 @dataclasses.dataclass
@@ -40,10 +58,34 @@ class Scene:
     vfov: float = 40.0
     aperture: float = 0.0
     focus: float = 10.0
+    spheres: np.ndarray = dataclasses.field(default_factory=lambda: np.zeros((0, 4), np.float32))  # cx cy cz r
+    sph_mat: np.ndarray = dataclasses.field(default_factory=lambda: np.zeros(0, np.int32))
+    mat_kind: np.ndarray = None  # (k,) int32, None = all Lambertian
+    fuzz: np.ndarray = None      # (k,) float32 (Metal)
+    ir: np.ndarray = None        # (k,) float32 (Dielectric)
 
     @property
     def num_tris(self) -> int:
         return int(self.verts.shape[0])
+
+    @property
+    def num_spheres(self) -> int:
+        return int(np.asarray(self.spheres).reshape(-1, 4).shape[0])
+
+    @property
+    def lambertian_triangles(self) -> bool:
+        """True when hipptUploadMesh / the v1 file format can carry the scene."""
+        return self.num_spheres == 0 and (self.mat_kind is None or not np.any(np.asarray(self.mat_kind)))
+
+    def materials(self) -> np.ndarray:
+        """Structured array of MATERIAL_DTYPE, one per material."""
+        k = int(np.asarray(self.albedo).reshape(-1, 3).shape[0])
+        m = np.zeros(k, MATERIAL_DTYPE)
+        m["albedo"] = np.asarray(self.albedo, np.float32).reshape(-1, 3)
+        m["kind"] = 0 if self.mat_kind is None else np.asarray(self.mat_kind, np.int32)
+        m["fuzz"] = 0.0 if self.fuzz is None else np.asarray(self.fuzz, np.float32)
+        m["ir"] = 1.0 if self.ir is None else np.asarray(self.ir, np.float32)
+        return m
 
 
 def _quad(a, b, c, d):
@@ -130,7 +172,76 @@ def blob70k() -> Scene:
                  albedo=np.asarray([WHITE, GREEN, RED], dtype=np.float32))
 
 
-SCENES = {"cornell34": cornell34, "blob70k": blob70k}
+def random_scene(seed: int = 2024) -> Scene:
+    """RayTracer.h random_scene (:599-643) drawn from numpy's PCG64 (seeded), camera of
+    RenderWorker::render (RayTracerFboItem.cpp:50-56: (13,2,3) -> 0, vfov 20, aperture 0.1,
+    focus 10)."""
+    rng = np.random.default_rng(seed)
+    rd = rng.random
+    spheres, mats = [], []
+
+    def add(c, r, kind, albedo=(0.0, 0.0, 0.0), fuzz=0.0, ir=1.0):
+        spheres.append((*c, r))
+        mats.append((kind, albedo, min(fuzz, 1.0) if kind == MAT_METAL else fuzz, ir))
+
+    add((0.0, -1000.0, 0.0), 1000.0, MAT_LAMBERTIAN, (0.5, 0.5, 0.5))
+    for a in range(-11, 11):
+        for b in range(-11, 11):
+            choose = rd()
+            c = (a + 0.9 * rd(), 0.2, b + 0.9 * rd())
+            if np.sqrt((c[0] - 4.0) ** 2 + (c[1] - 0.2) ** 2 + c[2] ** 2) <= 0.9:
+                continue
+            if choose < 0.8:
+                alb = tuple(float(rd() * rd()) for _ in range(3))
+                add(c, 0.2, MAT_LAMBERTIAN, alb)
+            elif choose < 0.95:
+                alb = tuple(float(0.5 + 0.5 * rd()) for _ in range(3))
+                add(c, 0.2, MAT_METAL, alb, fuzz=0.5 * rd())
+            else:
+                add(c, 0.2, MAT_DIELECTRIC, (1.0, 1.0, 1.0), ir=1.5)
+    add((0.0, 1.0, 0.0), 1.0, MAT_DIELECTRIC, (1.0, 1.0, 1.0), ir=1.5)
+    add((-4.0, 1.0, 0.0), 1.0, MAT_LAMBERTIAN, (0.4, 0.2, 0.1))
+    add((4.0, 1.0, 0.0), 1.0, MAT_METAL, (0.7, 0.6, 0.5), fuzz=0.0)
+    return _sphere_scene("random_scene", spheres, mats)
+
+
+def _sphere_scene(name, spheres, mats, verts=None, tri_mat=None, **cam) -> Scene:
+    kw = dict(lookfrom=(13.0, 2.0, 3.0), lookat=(0.0, 0.0, 0.0), vup=(0.0, 1.0, 0.0), vfov=20.0, aperture=0.1,
+              focus=10.0)
+    kw.update(cam)
+    return Scene(
+        name=name,
+        verts=np.zeros((0, 9), np.float32) if verts is None else np.ascontiguousarray(verts, np.float32),
+        tri_mat=np.zeros(0, np.int32) if tri_mat is None else np.asarray(tri_mat, np.int32),
+        albedo=np.asarray([m[1] for m in mats], np.float32).reshape(-1, 3),
+        spheres=np.asarray(spheres, np.float64).astype(np.float32).reshape(-1, 4),
+        sph_mat=np.arange(len(spheres), dtype=np.int32) if len(spheres) == len(mats) else None,
+        mat_kind=np.asarray([m[0] for m in mats], np.int32),
+        fuzz=np.asarray([m[2] for m in mats], np.float32),
+        ir=np.asarray([m[3] for m in mats], np.float32),
+        **kw,
+    )
+
+
+def cornell_mixed() -> Scene:
+    """Cornell walls + short white box, metal tall box, glass and fuzzy-metal spheres."""
+    tris, tmat = _walls()
+    short = _box((130, 0, 65), (295, 165, 230))
+    tall = _box((265, 0, 295), (430, 330, 460))
+    tris = tris + short + tall
+    tmat = tmat + [0] * len(short) + [3] * len(tall)
+    mats = [(MAT_LAMBERTIAN, WHITE, 0.0, 1.0), (MAT_LAMBERTIAN, GREEN, 0.0, 1.0), (MAT_LAMBERTIAN, RED, 0.0, 1.0),
+            (MAT_METAL, (0.8, 0.85, 0.88), 0.05, 1.0), (MAT_DIELECTRIC, (1.0, 1.0, 1.0), 0.0, 1.5),
+            (MAT_METAL, (0.9, 0.6, 0.3), 0.3, 1.0)]
+    sc = _sphere_scene("cornell_mixed", [], mats, verts=np.asarray(tris, np.float64).astype(np.float32),
+                       tri_mat=tmat, lookfrom=(278.0, 278.0, -800.0), lookat=(278.0, 278.0, 0.0), vfov=40.0,
+                       aperture=0.0, focus=10.0)
+    sc.spheres = np.asarray([(212.5, 245.0, 147.5, 80.0), (420.0, 60.0, 150.0, 60.0)], np.float32)
+    sc.sph_mat = np.asarray([4, 5], np.int32)
+    return sc
+
+
+SCENES = {"cornell34": cornell34, "blob70k": blob70k, "random_scene": random_scene, "cornell_mixed": cornell_mixed}
 
 
 def get_scene(name: str) -> Scene:
@@ -141,11 +252,65 @@ def get_scene(name: str) -> Scene:
 
 
 def write_scene_file(scene: Scene, path: str) -> None:
-    """Binary scene file read by oracle/ref_harness.cpp (load_scene)."""
+    """Binary scene file read by oracle/ref_harness.cpp (load_scene): v1 for Lambertian
+    triangle scenes, v2 otherwise."""
+    cam = list(scene.lookfrom) + list(scene.lookat) + list(scene.vup) + [scene.vfov, scene.aperture, scene.focus]
     with open(path, "wb") as f:
-        f.write(struct.pack("<3i", SCENE_MAGIC, scene.num_tris, len(scene.albedo)))
-        f.write(np.ascontiguousarray(scene.verts, dtype="<f4").tobytes())
-        f.write(np.ascontiguousarray(scene.tri_mat, dtype="<i4").tobytes())
-        f.write(np.ascontiguousarray(scene.albedo, dtype="<f4").tobytes())
-        cam = list(scene.lookfrom) + list(scene.lookat) + list(scene.vup) + [scene.vfov, scene.aperture, scene.focus]
+        if scene.lambertian_triangles:
+            f.write(struct.pack("<3i", SCENE_MAGIC, scene.num_tris, len(scene.albedo)))
+            f.write(np.ascontiguousarray(scene.verts, dtype="<f4").tobytes())
+            f.write(np.ascontiguousarray(scene.tri_mat, dtype="<i4").tobytes())
+            f.write(np.ascontiguousarray(scene.albedo, dtype="<f4").tobytes())
+        else:
+            mats = scene.materials()
+            f.write(struct.pack("<4i", SCENE_MAGIC_V2, scene.num_tris, scene.num_spheres, len(mats)))
+            f.write(np.ascontiguousarray(scene.verts, dtype="<f4").tobytes())
+            f.write(np.ascontiguousarray(scene.tri_mat, dtype="<i4").tobytes())
+            f.write(np.ascontiguousarray(scene.spheres, dtype="<f4").tobytes())
+            f.write(np.ascontiguousarray(scene.sph_mat, dtype="<i4").tobytes())
+            f.write(mats.tobytes())
         f.write(struct.pack("<12d", *cam))
+
+
+def load_scene_file(path: str, name: str = None) -> Scene:
+    """Reads a v1 or v2 scene file (write_scene_file, oracle/ref_harness.cpp random_scene)."""
+    with open(path, "rb") as f:
+        data = f.read()
+    magic = struct.unpack_from("<i", data, 0)[0]
+    off = 4
+    if magic == SCENE_MAGIC:
+        nt, nm = struct.unpack_from("<2i", data, off)
+        ns = 0
+        off += 8
+    elif magic == SCENE_MAGIC_V2:
+        nt, ns, nm = struct.unpack_from("<3i", data, off)
+        off += 12
+    else:
+        raise ValueError(f"{path}: not a scene file")
+
+    def take(dtype, count):
+        nonlocal off
+        a = np.frombuffer(data, dtype=dtype, count=count, offset=off).copy()
+        off += a.nbytes
+        return a
+
+    verts = take("<f4", nt * 9).reshape(-1, 9)
+    tri_mat = take("<i4", nt)
+    if magic == SCENE_MAGIC:
+        albedo = take("<f4", nm * 3).reshape(-1, 3)
+        mats = None
+        spheres, sph_mat = np.zeros((0, 4), np.float32), np.zeros(0, np.int32)
+    else:
+        spheres = take("<f4", ns * 4).reshape(-1, 4)
+        sph_mat = take("<i4", ns)
+        mats = take(MATERIAL_DTYPE, nm)
+        albedo = np.ascontiguousarray(mats["albedo"])
+    cam = struct.unpack_from("<12d", data, off)
+    sc = Scene(name=name or os.path.splitext(os.path.basename(path))[0], verts=verts, tri_mat=tri_mat, albedo=albedo,
+               lookfrom=tuple(cam[0:3]), lookat=tuple(cam[3:6]), vup=tuple(cam[6:9]), vfov=cam[9], aperture=cam[10],
+               focus=cam[11], spheres=spheres, sph_mat=sph_mat)
+    if mats is not None:
+        sc.mat_kind = np.ascontiguousarray(mats["kind"])
+        sc.fuzz = np.ascontiguousarray(mats["fuzz"])
+        sc.ir = np.ascontiguousarray(mats["ir"])
+    return sc

@@ -2,18 +2,24 @@
 
 Run in the development container only (needs /root/reference to build oracle/_ref):
 
-    make -C oracle ref && python tests/golden/make_golden.py
+    make -C oracle ref && python tests/golden/make_golden.py [TARGET ...]
 
-Outputs (committed; data only — inputs and the reference's outputs):
-  ref_functions.json    FP64 outputs of RayTracer.h Sphere::hit, AABB::hit, surrounding_box,
-                        Camera::get_ray (aperture 0), reflect/refract, degrees_to_radians on
-                        seeded inputs, plus BVHNode closest hits (harness Triangle) on cornell34
-  ref_bvh_blob70k.json  BVHNode closest hits on blob70k
-  ref_converge_<scene>_<W>x<H>_<spp>.npy  per-pixel mean (3) and variance (3) of the reference
-                        ray_color radiance, for statistical agreement tests
+Targets (default: all; the converged images are Monte-Carlo estimates, so regenerating
+them changes the bytes but not the statistics the tests check):
+  functions     ref_functions.json: FP64 outputs of RayTracer.h Sphere::hit, AABB::hit,
+                surrounding_box, Camera::get_ray (aperture 0), reflect/refract,
+                degrees_to_radians on seeded inputs, plus BVHNode closest hits (harness
+                Triangle) on cornell34; ref_bvh_blob70k.json: BVHNode closest hits on blob70k
+  converge      ref_converge_<scene>_<W>x<H>_<spp>.npy: per-pixel mean (3) and variance (3)
+                of the reference ray_color radiance, for statistical agreement tests
+  random_scene  ref_random_scene.scene: one random_scene() (RayTracer.h:599-643) as the
+                reference generated it (its RNG is nondeterministic, so this target only
+                runs when the file is missing or --force is given)
+Fixtures are data only: inputs and the reference's outputs.
 """
 from __future__ import annotations
 
+import argparse
 import json
 import os
 import subprocess
@@ -29,13 +35,19 @@ sys.path[:0] = [os.path.join(REPO, "qt-raytracer_amd"), os.path.join(REPO, "orac
 from hippt import scenes  # noqa: E402
 import pyoracle  # noqa: E402
 
-CONVERGE = [("cornell34", 64, 64, 4096, 8), ("blob70k", 32, 32, 1024, 8)]
+RANDOM_SCENE = os.path.join(HERE, "ref_random_scene.scene")
+# (scene, W, H, spp, depth); "ref_random_scene" is the reference-generated sphere scene
+CONVERGE = [("cornell34", 64, 64, 4096, 8), ("blob70k", 32, 32, 1024, 8),
+            ("ref_random_scene", 48, 27, 2048, 8), ("cornell_mixed", 48, 48, 2048, 8)]
 
 
-def main() -> None:
-    if not os.path.exists(pyoracle.REF_HARNESS_STRICT):
-        raise SystemExit("oracle/_ref not built: make -C oracle ref (needs /root/reference)")
-    tmp = tempfile.mkdtemp()
+def scene_by_name(name):
+    if name == "ref_random_scene":
+        return scenes.load_scene_file(RANDOM_SCENE, name)
+    return scenes.get_scene(name)
+
+
+def make_functions(tmp) -> None:
     paths = {}
     for name in ("cornell34", "blob70k"):
         paths[name] = os.path.join(tmp, name + ".scene")
@@ -48,13 +60,37 @@ def main() -> None:
         blob = json.load(f)
     with open(os.path.join(HERE, "ref_bvh_blob70k.json"), "w") as f:
         json.dump({"bvh_closest": blob["bvh_closest"]}, f)
+
+
+def make_converge(tmp, only=None) -> None:
     for name, w, h, spp, depth in CONVERGE:
+        if only and name not in only:
+            continue
+        path = os.path.join(tmp, name + ".scene")
+        scenes.write_scene_file(scene_by_name(name), path)
         raw = os.path.join(tmp, f"{name}.f32")
-        subprocess.run([pyoracle.REF_HARNESS, "converge", paths[name], str(w), str(h), str(spp), str(depth), raw,
+        subprocess.run([pyoracle.REF_HARNESS, "converge", path, str(w), str(h), str(spp), str(depth), raw,
                         str(os.cpu_count() or 1)], check=True)
         img = np.fromfile(raw, dtype=np.float32).reshape(h, w, 6)
         np.save(os.path.join(HERE, f"ref_converge_{name}_{w}x{h}_{spp}.npy"), img)
         print(name, "mean radiance", img[..., :3].mean(axis=(0, 1)))
+
+
+def main() -> None:
+    ap = argparse.ArgumentParser()
+    ap.add_argument("targets", nargs="*", default=["functions", "random_scene", "converge"])
+    ap.add_argument("--scenes", nargs="*", help="converge only these scenes")
+    ap.add_argument("--force", action="store_true", help="regenerate ref_random_scene.scene")
+    a = ap.parse_args()
+    if not os.path.exists(pyoracle.REF_HARNESS_STRICT):
+        raise SystemExit("oracle/_ref not built: make -C oracle ref (needs /root/reference)")
+    tmp = tempfile.mkdtemp()
+    if "functions" in a.targets:
+        make_functions(tmp)
+    if "random_scene" in a.targets and (a.force or not os.path.exists(RANDOM_SCENE)):
+        subprocess.run([pyoracle.REF_HARNESS_STRICT, "random_scene", RANDOM_SCENE], check=True)
+    if "converge" in a.targets:
+        make_converge(tmp, a.scenes)
 
 
 if __name__ == "__main__":
