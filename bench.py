@@ -52,7 +52,11 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--scene", default="cornell34", choices=["cornell34", "blob70k"])
+    p.add_argument("--scene", default="cornell34",
+                   choices=["cornell34", "blob70k", "random_scene", "cornell_mixed"])
+    p.add_argument("--path-mode", default="megakernel", choices=["megakernel", "wavefront"],
+                   help="BASELINE configs[4] A/B: persistent megakernel or wavefront kernels")
+    p.add_argument("--wavefront-slots", type=int, default=None)
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=1080)
     p.add_argument("--spp", type=int, default=64)
@@ -174,6 +178,9 @@ def main():
         pt.setOption(hippt.OPT_CHUNK, args.chunk)
     if args.scratch_mb is not None:
         pt.setOption(hippt.OPT_SCRATCH_MB, args.scratch_mb)
+    pt.setOption(hippt.OPT_PATH_MODE, 1 if args.path_mode == "wavefront" else 0)
+    if args.wavefront_slots is not None:
+        pt.setOption(hippt.OPT_WAVEFRONT_SLOTS, args.wavefront_slots)
     pt.uploadMesh(scene)
     if not pt.initialize(args.width, args.height):
         raise SystemExit(pt.lastError())
@@ -227,6 +234,8 @@ def main():
     mean_launch_ms = st["traceMs"] / max(1, st["traceLaunches"])
     achieved = alg_bytes_launch / (mean_launch_ms * 1e-3) / 1e9 if mean_launch_ms > 0 else 0.0
     workload = f"{args.scene} {args.width}x{args.height} {args.spp}spp depth{args.depth}"
+    if args.path_mode == "wavefront":
+        workload += " wavefront"
     traffic = load_pmc(args, workload)
 
     if rank == 0:
@@ -248,7 +257,8 @@ def main():
             "config": {
                 "workload": workload + " (BASELINE configs[1])" if args.scene == "cornell34" and args.width == 1920
                 and args.height == 1080 and args.spp == 64 and args.depth == 8 else workload,
-                "scene": args.scene, "triangles": scene.num_tris, "width": args.width, "height": args.height,
+                "scene": args.scene, "triangles": scene.num_tris, "spheres": scene.num_spheres,
+                "path_mode": args.path_mode, "width": args.width, "height": args.height,
                 "spp": args.spp, "max_depth": args.depth, "parallelism": f"row-bands x{world}",
                 "segments_per_step": segments // max(1, args.steps),
                 "pixel_samples_per_step": samples // max(1, args.steps),
@@ -263,7 +273,8 @@ def main():
             "roofline": {
                 "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "mesh_kernel", "mean_launch_ms": round(mean_launch_ms, 4),
+                "kernel": "mesh_kernel" if args.path_mode == "megakernel" else "wf_extend+wf_shade+wf_generate",
+                "mean_launch_ms": round(mean_launch_ms, 4),
                 "launches_per_step": launches,
                 "alg_bytes_per_launch": int(alg_bytes_launch),
                 "node_visits_per_step": counted["nodeVisits"], "tri_tests_per_step": counted["triTests"],
