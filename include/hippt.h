@@ -96,6 +96,22 @@ bool hipptUploadScene(const float *verts, const int *triMaterial, int numTris, c
                       const double lookfrom[3], const double lookat[3], const double vup[3], double vfovDeg,
                       double aperture, double focusDist, const char **errorMessage);
 
+/* Triangle mesh read from a Wavefront OBJ or PLY file (the reference has no mesh input):
+ * verts = numTris*9 floats (polygons fan-triangulated), triGroup = numTris ints in
+ * [0, numGroups): OBJ `usemtl` groups in order of first use (groupNames[g]; "" = faces before
+ * any usemtl), PLY: 0.  Feed verts/triGroup to hipptUploadMesh/hipptUploadScene with one
+ * material per group.  Library-owned; release with hipptFreeMesh. */
+typedef struct {
+    float *verts;
+    int *triGroup;
+    int numTris;
+    int numGroups;
+    const char *const *groupNames;
+    void *owner_;
+} hipptMesh;
+bool hipptReadMesh(const char *path, hipptMesh *out, const char **errorMessage);
+void hipptFreeMesh(hipptMesh *mesh);
+
 /* Optional: replace the camera by a prebuilt one (used as-is, whatever the aspect). */
 bool hipptSetCamera(const hipptCamera *camera, const char **errorMessage);
 

@@ -22,6 +22,7 @@
 #include <vector>
 
 #include "bvh_builder.h"
+#include "mesh_io.h"
 #include "hippt_device.h"
 #include "hippt_wavefront.h"
 
@@ -704,6 +705,39 @@ extern "C" bool hipptUploadMesh(const float *verts, const int *triMaterial, int 
                                         1.0f};
     return hipptUploadScene(verts, triMaterial, numTris, nullptr, nullptr, 0, mats.data(), numMaterials, lookfrom,
                             lookat, vup, vfovDeg, aperture, focusDist, err);
+}
+
+namespace {
+struct MeshOwner {
+    hippt::MeshData data;
+    std::vector<const char *> names;
+};
+}  // namespace
+
+extern "C" bool hipptReadMesh(const char *path, hipptMesh *out, const char **err) {
+    if (!path || !out) return fail(err, "null argument");
+    std::memset(out, 0, sizeof(*out));
+    auto *own = new MeshOwner;
+    std::string msg;
+    if (!hippt::read_mesh(path, own->data, msg)) {
+        delete own;
+        std::lock_guard<std::mutex> g(S().mu);
+        return fail(err, msg);
+    }
+    for (const std::string &n : own->data.groups) own->names.push_back(n.c_str());
+    out->verts = own->data.verts.data();
+    out->triGroup = own->data.group.data();
+    out->numTris = int(own->data.group.size());
+    out->numGroups = int(own->data.groups.size());
+    out->groupNames = own->names.data();
+    out->owner_ = own;
+    return true;
+}
+
+extern "C" void hipptFreeMesh(hipptMesh *mesh) {
+    if (!mesh) return;
+    delete static_cast<MeshOwner *>(mesh->owner_);
+    std::memset(mesh, 0, sizeof(*mesh));
 }
 
 extern "C" bool hipptSetCamera(const hipptCamera *camera, const char **err) {

@@ -39,7 +39,8 @@ OPT_WAVEFRONT_SLOTS = 9
 EXPORTS = (
     "cudaPathTracerInit", "cudaPathTracerRender", "cudaPathTracerShutdown",
     "hipPathTracerInit", "hipPathTracerRender", "hipPathTracerShutdown",
-    "hipptBuildCamera", "hipptUseBuiltinScene", "hipptUploadMesh", "hipptUploadScene", "hipptSetCamera",
+    "hipptBuildCamera", "hipptUseBuiltinScene", "hipptUploadMesh", "hipptUploadScene", "hipptReadMesh",
+    "hipptFreeMesh", "hipptSetCamera",
     "hipptDeviceCount", "hipptSetDevices", "hipptSetRowRange",
     "hipptRenderFrames", "hipptRenderFramesAsync", "hipptSynchronize", "hipptReadback",
     "hipptResetAccumulation", "hipptGetStats", "hipptResetStats", "hipptGetCounters", "hipptSetOption",
@@ -60,6 +61,13 @@ class Camera(ctypes.Structure):
 
     def as_array(self) -> np.ndarray:
         return np.frombuffer(bytes(self), dtype=np.float32).copy()
+
+
+class Mesh(ctypes.Structure):
+    """hipptMesh (include/hippt.h)."""
+    _fields_ = [("verts", ctypes.POINTER(ctypes.c_float)), ("triGroup", ctypes.POINTER(ctypes.c_int)),
+                ("numTris", ctypes.c_int), ("numGroups", ctypes.c_int),
+                ("groupNames", ctypes.POINTER(ctypes.c_char_p)), ("owner_", ctypes.c_void_p)]
 
 
 class Stats(ctypes.Structure):
@@ -112,6 +120,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
         c_double, c_double, c_double, pp_char)
     sig("hipptUploadScene", c_bool, p_float, p_int, c_int, p_float, p_int, c_int, ctypes.c_void_p, c_int, p_double,
         p_double, p_double, c_double, c_double, c_double, pp_char)
+    sig("hipptReadMesh", c_bool, c_char_p, ctypes.POINTER(Mesh), pp_char)
+    sig("hipptFreeMesh", None, ctypes.POINTER(Mesh))
     sig("hipptSetCamera", c_bool, ctypes.POINTER(Camera), pp_char)
     sig("hipptDeviceCount", c_int)
     sig("hipptSetDevices", c_bool, p_int, c_int, pp_char)
@@ -146,6 +156,23 @@ def _ptr(a: np.ndarray, ct):
 
 def _d3(v) -> ctypes.Array:
     return (ctypes.c_double * 3)(*[float(x) for x in v])
+
+
+def read_mesh(path: str):
+    """hipptReadMesh: (verts (n, 9) float32, tri_group (n,) int32, group names) of an OBJ/PLY file."""
+    lib = load_library()
+    m = Mesh()
+    e = ctypes.c_char_p()
+    if not lib.hipptReadMesh(os.fsencode(path), ctypes.byref(m), ctypes.byref(e)):
+        raise HipptError(_err(e, f"cannot read {path}"))
+    try:
+        n = m.numTris
+        verts = np.ctypeslib.as_array(m.verts, shape=(n * 9,)).reshape(n, 9).copy()
+        groups = np.ctypeslib.as_array(m.triGroup, shape=(n,)).copy()
+        names = [m.groupNames[g].decode() for g in range(m.numGroups)]
+    finally:
+        lib.hipptFreeMesh(ctypes.byref(m))
+    return verts, groups, names
 
 
 def build_camera(lookfrom, lookat, vup, vfov, aspect, aperture, focus) -> Camera:

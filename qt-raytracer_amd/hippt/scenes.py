@@ -314,3 +314,69 @@ def load_scene_file(path: str, name: str = None) -> Scene:
         sc.fuzz = np.ascontiguousarray(mats["fuzz"])
         sc.ir = np.ascontiguousarray(mats["ir"])
     return sc
+
+
+def write_obj(scene: Scene, path: str, style: str = "plain") -> None:
+    """Triangles of `scene` as a Wavefront OBJ file: one `usemtl m<k>` group per material,
+    coordinates printed with 9 significant digits (they read back to the same float32).
+    style "quads": consecutive same-material pairs (a, b, c) (a, c, d) — the layout of every
+    quad here — become one quad `f a b/b c//c d/d/d`; "relative": negative vertex indices."""
+    v = np.asarray(scene.verts, np.float32).reshape(-1, 3)
+    mats = np.asarray(scene.tri_mat)
+    nv = len(v)
+
+    def ref(k):  # 1-based vertex k
+        return str(k - nv - 1) if style == "relative" else str(k)
+
+    with open(path, "w") as f:
+        f.write(f"# {scene.name}: {scene.num_tris} triangles\n")
+        for x, y, z in v:
+            f.write(f"v {x:.9g} {y:.9g} {z:.9g}\n")
+        cur, t, n = None, 0, scene.num_tris
+        while t < n:
+            if mats[t] != cur:
+                cur = mats[t]
+                f.write(f"usemtl m{cur}\n")
+            a, b, c = 3 * t + 1, 3 * t + 2, 3 * t + 3
+            if style == "quads" and t + 1 < n and mats[t + 1] == cur:
+                d = 3 * t + 6
+                f.write(f"f {a} {b}/{b} {c}//{c} {d}/{d}/{d}\n")
+                t += 2
+            else:
+                f.write(f"f {ref(a)} {ref(b)} {ref(c)}\n")
+                t += 1
+
+
+def write_ply(scene: Scene, path: str, fmt: str = "binary_little_endian") -> None:
+    """Triangles of `scene` as a PLY file (vertex x, y, z float; face list uchar int), one
+    vertex per corner; fmt ascii / binary_little_endian / binary_big_endian."""
+    v = np.asarray(scene.verts, np.float32).reshape(-1, 3)
+    n = scene.num_tris
+    head = (f"ply\nformat {fmt} 1.0\ncomment {scene.name}\nelement vertex {len(v)}\n"
+            "property float x\nproperty float y\nproperty float z\n"
+            f"element face {n}\nproperty list uchar int vertex_indices\nend_header\n")
+    with open(path, "wb") as f:
+        f.write(head.encode())
+        if fmt == "ascii":
+            lines = [f"{x:.9g} {y:.9g} {z:.9g}" for x, y, z in v]
+            lines += [f"3 {3 * t} {3 * t + 1} {3 * t + 2}" for t in range(n)]
+            f.write(("\n".join(lines) + "\n").encode())
+        else:
+            e = "<" if fmt == "binary_little_endian" else ">"
+            f.write(v.astype(e + "f4").tobytes())
+            face = np.zeros(n, dtype=[("c", "u1"), ("i", e + "i4", (3,))])
+            face["c"] = 3
+            face["i"] = np.arange(3 * n, dtype=np.int64).reshape(n, 3)
+            f.write(face.tobytes())
+
+
+def from_mesh_file(path: str, albedo=None, name: str = None, **camera) -> Scene:
+    """Scene from an OBJ/PLY file read by libhippt (hipptReadMesh): one Lambertian material per
+    OBJ `usemtl` group (albedo: (groups, 3), default white 0.73), camera keywords as Scene's
+    (default: the Cornell camera)."""
+    from hippt import read_mesh  # the library reader, no Python fallback
+    verts, groups, names = read_mesh(path)
+    k = max(1, len(names))
+    alb = np.tile(np.float32(WHITE), (k, 1)) if albedo is None else np.asarray(albedo, np.float32).reshape(k, 3)
+    return Scene(name=name or os.path.splitext(os.path.basename(path))[0], verts=verts,
+                 tri_mat=groups.astype(np.int32), albedo=alb, **camera)
