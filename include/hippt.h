@@ -133,6 +133,14 @@ bool hipptRenderFrames(int firstFrame, int count, int maxDepth, const unsigned i
 /* Enqueues the same work without waiting and without a device-to-host copy. */
 bool hipptRenderFramesAsync(int firstFrame, int count, int maxDepth, const char **errorMessage);
 bool hipptSynchronize(const char **errorMessage);
+/* Interactive hand-off (replaces the blocking full-frame copy of CudaPathTracerKernel.cu:261-265
+ * for hosts that can show the previous image): enqueues the frames and a copy of the ARGB image
+ * into one of two library-owned pinned frames, and returns without waiting. */
+bool hipptRenderFramesPresent(int firstFrame, int count, int maxDepth, const char **errorMessage);
+/* Never blocks: *hostPixels = the newest presented image whose copy has completed (null if
+ * none yet), *frames = the frame count accumulated in it.  The image stays valid until the
+ * second hipptRenderFramesPresent call after the one that produced it (double buffering). */
+bool hipptLatestFrame(const unsigned int **hostPixels, int *frames, const char **errorMessage);
 /* Copies the current image (ARGB, W*H) and/or accumulation buffer (RGBA float, W*H*4)
  * of the process's row range into caller memory; rows outside the range are untouched. */
 bool hipptReadback(unsigned int *pixels, float *accum, const char **errorMessage);

@@ -63,9 +63,10 @@ struct Ctx {
     int cus = 0;
     long long occKey = -1;  // occupancy cached per (scene version, depth, lds, full)
     int meshBlocksPerCu[2] = {0, 0};
-    std::vector<EventPair> pool;                         // reusable events
+    std::vector<EventPair> pool;                         // every timing event pair created
+    std::vector<EventPair> freeEv;                       // pairs not in flight
     std::vector<std::pair<int, EventPair>> pending;      // (0 trace / 1 combine, events)
-    size_t poolUsed = 0;
+    hipEvent_t presentEv[2] = {nullptr, nullptr};        // band copy into State::present[b] done
 };
 
 struct SceneHost {
@@ -89,6 +90,14 @@ struct State {
     std::vector<Ctx> ctxs;
     unsigned *host = nullptr;  // pinned W*H ARGB frame (library-owned, as gState.hostOutput)
     size_t hostCount = 0;
+    // asynchronous hand-off (hipptRenderFramesPresent / hipptLatestFrame): two pinned frames
+    unsigned *present[2] = {nullptr, nullptr};
+    int presentNext = 0;                 // buffer the next present call writes
+    bool presentPending[2] = {false, false};
+    long long presentSeq[2] = {-1, -1};  // present call number of the buffer's contents
+    int presentFrames[2] = {0, 0};       // frames accumulated in that image
+    long long presentCalls = 0;
+    int latest = -1;                     // newest completed buffer
     SceneHost scene;
     char error[256] = {0};
     // options
@@ -205,6 +214,8 @@ void destroy_ctx(Ctx &c) {
         (void)hipEventDestroy(e.a);
         (void)hipEventDestroy(e.b);
     }
+    for (hipEvent_t e : c.presentEv)
+        if (e) (void)hipEventDestroy(e);
     if (c.stream) (void)hipStreamDestroy(c.stream);
     c = Ctx();
 }
@@ -216,17 +227,54 @@ void destroy_all() {
     if (s.host) (void)hipHostFree(s.host);
     s.host = nullptr;
     s.hostCount = 0;
+    for (int b = 0; b < 2; ++b) {
+        if (s.present[b]) (void)hipHostFree(s.present[b]);
+        s.present[b] = nullptr;
+        s.presentPending[b] = false;
+        s.presentSeq[b] = -1;
+    }
+    s.presentNext = 0;
+    s.latest = -1;
     s.ready = false;
 }
 
 bool next_events(Ctx &c, EventPair &ev, const char **err) {
-    if (c.poolUsed == c.pool.size()) {
+    if (c.freeEv.empty()) {
         EventPair e;
         HIP_TRY(hipEventCreate(&e.a));
         HIP_TRY(hipEventCreate(&e.b));
         c.pool.push_back(e);
+        c.freeEv.push_back(e);
     }
-    ev = c.pool[c.poolUsed++];
+    ev = c.freeEv.back();
+    c.freeEv.pop_back();
+    return true;
+}
+
+// Adds a finished launch's event time to the stats and recycles its events.
+bool account(const std::pair<int, EventPair> &pe, Ctx &c, const char **err) {
+    State &s = S();
+    float ms = 0.0f;
+    HIP_TRY(hipEventElapsedTime(&ms, pe.second.a, pe.second.b));
+    if (pe.first == 0) {
+        s.traceMs += ms;
+        ++s.traceLaunches;
+    } else {
+        s.combineMs += ms;
+        ++s.combineLaunches;
+    }
+    c.freeEv.push_back(pe.second);
+    return true;
+}
+
+// Non-blocking: accounts the launches (in stream order) that have already finished.
+bool harvest_locked(Ctx &c, const char **err) {
+    size_t done = 0;
+    while (done < c.pending.size() && hipEventQuery(c.pending[done].second.b) == hipSuccess) {
+        if (!account(c.pending[done], c, err)) return false;
+        ++done;
+    }
+    c.pending.erase(c.pending.begin(), c.pending.begin() + long(done));
     return true;
 }
 
@@ -508,19 +556,9 @@ bool sync_locked(const char **err) {
     for (Ctx &c : s.ctxs) {
         HIP_TRY(hipSetDevice(c.device));
         HIP_TRY(hipStreamSynchronize(c.stream));
-        for (auto &pe : c.pending) {
-            float ms = 0.0f;
-            HIP_TRY(hipEventElapsedTime(&ms, pe.second.a, pe.second.b));
-            if (pe.first == 0) {
-                s.traceMs += ms;
-                ++s.traceLaunches;
-            } else {
-                s.combineMs += ms;
-                ++s.combineLaunches;
-            }
-        }
+        for (auto &pe : c.pending)
+            if (!account(pe, c, err)) return false;
         c.pending.clear();
-        c.poolUsed = 0;
     }
     return true;
 }
@@ -790,6 +828,58 @@ extern "C" bool hipptRenderFramesAsync(int firstFrame, int count, int maxDepth, 
 extern "C" bool hipptSynchronize(const char **err) {
     std::lock_guard<std::mutex> g(S().mu);
     return sync_locked(err);
+}
+
+extern "C" bool hipptRenderFramesPresent(int firstFrame, int count, int maxDepth, const char **err) {
+    std::lock_guard<std::mutex> g(S().mu);
+    State &s = S();
+    if (!enqueue_locked(firstFrame, count, maxDepth, false, err)) return false;
+    const int b = s.presentNext;
+    if (!s.present[b])
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.present[b]), s.hostCount * sizeof(unsigned),
+                              hipHostMallocPortable));
+    for (Ctx &c : s.ctxs) {
+        HIP_TRY(hipSetDevice(c.device));
+        if (!c.presentEv[b]) HIP_TRY(hipEventCreateWithFlags(&c.presentEv[b], hipEventDisableTiming));
+        const size_t bandPixels = size_t(c.y1 - c.y0) * size_t(s.width);
+        if (bandPixels)
+            HIP_TRY(hipMemcpyAsync(s.present[b] + size_t(c.y0) * size_t(s.width), c.out, bandPixels * sizeof(uint32_t),
+                                   hipMemcpyDeviceToHost, c.stream));
+        HIP_TRY(hipEventRecord(c.presentEv[b], c.stream));
+        if (!harvest_locked(c, err)) return false;
+    }
+    if (s.latest == b) s.latest = -1;  // its image is being replaced
+    s.presentPending[b] = true;
+    s.presentSeq[b] = s.presentCalls++;
+    s.presentFrames[b] = firstFrame + count;
+    s.presentNext = b ^ 1;
+    return true;
+}
+
+extern "C" bool hipptLatestFrame(const unsigned int **hostPixels, int *frames, const char **err) {
+    std::lock_guard<std::mutex> g(S().mu);
+    State &s = S();
+    if (!s.ready) return fail(err, "HIP path tracer not initialized");
+    for (int b = 0; b < 2; ++b) {
+        if (!s.presentPending[b]) continue;
+        bool done = true;
+        for (Ctx &c : s.ctxs) {
+            HIP_TRY(hipSetDevice(c.device));
+            const hipError_t q = hipEventQuery(c.presentEv[b]);
+            if (q == hipErrorNotReady) {
+                done = false;
+                break;
+            }
+            if (q != hipSuccess) return fail(err, std::string("hipEventQuery: ") + hipGetErrorString(q));
+        }
+        if (done) {
+            s.presentPending[b] = false;
+            if (s.latest < 0 || s.presentSeq[b] > s.presentSeq[s.latest]) s.latest = b;
+        }
+    }
+    if (hostPixels) *hostPixels = s.latest >= 0 ? s.present[s.latest] : nullptr;
+    if (frames) *frames = s.latest >= 0 ? s.presentFrames[s.latest] : 0;
+    return true;
 }
 
 extern "C" bool hipptReadback(unsigned int *pixels, float *accum, const char **err) {

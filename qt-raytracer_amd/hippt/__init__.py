@@ -42,7 +42,8 @@ EXPORTS = (
     "hipptBuildCamera", "hipptUseBuiltinScene", "hipptUploadMesh", "hipptUploadScene", "hipptReadMesh",
     "hipptFreeMesh", "hipptSetCamera",
     "hipptDeviceCount", "hipptSetDevices", "hipptSetRowRange",
-    "hipptRenderFrames", "hipptRenderFramesAsync", "hipptSynchronize", "hipptReadback",
+    "hipptRenderFrames", "hipptRenderFramesAsync", "hipptSynchronize", "hipptRenderFramesPresent",
+    "hipptLatestFrame", "hipptReadback",
     "hipptResetAccumulation", "hipptGetStats", "hipptResetStats", "hipptGetCounters", "hipptSetOption",
     "hipptGetOption",
     "hipptLastError", "hipptBvhBuild", "hipptBvhNodeCount", "hipptBvhDepth", "hipptBvhCopy", "hipptBvhFree",
@@ -129,6 +130,8 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     sig("hipptRenderFrames", c_bool, c_int, c_int, c_int, pp_uint, pp_char)
     sig("hipptRenderFramesAsync", c_bool, c_int, c_int, c_int, pp_char)
     sig("hipptSynchronize", c_bool, pp_char)
+    sig("hipptRenderFramesPresent", c_bool, c_int, c_int, c_int, pp_char)
+    sig("hipptLatestFrame", c_bool, pp_uint, ctypes.POINTER(c_int), pp_char)
     sig("hipptReadback", c_bool, p_uint, p_float, pp_char)
     sig("hipptResetAccumulation", c_bool, pp_char)
     sig("hipptGetStats", c_bool, ctypes.POINTER(Stats))
@@ -276,6 +279,28 @@ class PathTracer:
             return False
         self._frame_index += int(samplesPerFrame)
         return True
+
+    def renderFramesPresent(self, samplesPerFrame: int, maxDepth: int) -> bool:  # noqa: N802
+        """Enqueues frames plus a copy into the next pinned hand-off frame; does not wait."""
+        e = ctypes.c_char_p()
+        if not self._lib.hipptRenderFramesPresent(self._frame_index, int(samplesPerFrame), int(maxDepth),
+                                                  ctypes.byref(e)):
+            self._last_error = _err(e, "HIP render failed")
+            return False
+        self._frame_index += int(samplesPerFrame)
+        return True
+
+    def latestFrame(self):  # noqa: N802
+        """Non-blocking: (ARGB (H, W) copy or None, frames accumulated in it)."""
+        e = ctypes.c_char_p()
+        px = ctypes.POINTER(ctypes.c_uint)()
+        n = ctypes.c_int()
+        if not self._lib.hipptLatestFrame(ctypes.byref(px), ctypes.byref(n), ctypes.byref(e)):
+            raise HipptError(_err(e, "latest frame failed"))
+        if not px:
+            return None, 0
+        h, w = self._height, self._width
+        return np.ctypeslib.as_array(px, shape=(h * w,)).reshape(h, w).copy(), n.value
 
     def synchronize(self) -> bool:
         e = ctypes.c_char_p()

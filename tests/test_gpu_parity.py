@@ -182,6 +182,28 @@ def test_general_kernel_equals_lambertian_kernel(pt):
     _assert_same(got[0], got[1], want[0], want[1])
 
 
+def test_present_hand_off_double_buffers(pt):
+    """hipptRenderFramesPresent / hipptLatestFrame: non-blocking hand-off of the newest image;
+    after a sync the latest frame is the last one presented and equals the accumulation."""
+    sc = scenes.cornell34()
+    pt.uploadMesh(sc)
+    w, h = 64, 48
+    assert pt.initialize(w, h)
+    assert pt.latestFrame() == (None, 0)
+    for _ in range(5):
+        assert pt.renderFramesPresent(2, 8), pt.lastError()
+        img, n = pt.latestFrame()  # whatever has finished; never waits
+        assert img is None or n in (2, 4, 6, 8, 10)
+    assert pt.synchronize()
+    img, n = pt.latestFrame()
+    assert n == 10
+    ora_px, _, _, _ = po.MeshScene(sc, w, h).frames(0, 10, 8)
+    assert np.array_equal(img, ora_px)
+    assert np.array_equal(pt.readback()[0], ora_px)
+    st = pt.stats()  # launches harvested without a sync are still accounted
+    assert st["traceLaunches"] == 5 and st["combineLaunches"] == 5
+
+
 def test_mesh_wave_threshold_and_chunk_do_not_change_results(pt):
     sc = scenes.cornell34()
     pt.uploadMesh(sc)
