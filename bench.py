@@ -3,9 +3,9 @@
 
 Workload (BASELINE.json configs[1]): Cornell-34 scene, 1920x1080, 64 spp, 8 bounces.
 One step = the whole workload once: 64 frames of every pixel (running-average accumulation,
-frames 0..63) through libhippt's C ABI.  With N GPUs (torchrun, one process per GPU) the
-image is split into N contiguous row bands, one per rank (strong scaling: the image is fixed);
-no collective touches the data path — ranks only meet at the barriers and the max-over-ranks
+frames 0..63) through libhippt's C ABI.  With N GPUs (torchrun, one process per GPU) rank r
+renders rows r, r+N, r+2N, ... (interleaved: contiguous bands differ in cost by up to 1.6x; the
+image is fixed, strong scaling); no collective touches the data path — ranks only meet at the barriers and the max-over-ranks
 of the timed interval (gloo, CPU).
 
 value = segments traced by all ranks in the K timed steps / max-over-ranks wall time, in
@@ -33,6 +33,8 @@ import sys
 import tempfile
 import time
 
+import numpy as np
+
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "qt-raytracer_amd"))
 
@@ -57,6 +59,8 @@ def parse():
     p.add_argument("--path-mode", default="megakernel", choices=["megakernel", "wavefront"],
                    help="BASELINE configs[4] A/B: persistent megakernel or wavefront kernels")
     p.add_argument("--wavefront-slots", type=int, default=None)
+    p.add_argument("--split", default="interleave", choices=["interleave", "bands"],
+                   help="rows per rank for N>1: interleaved (rank r: rows r, r+N, ...) or contiguous bands")
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=1080)
     p.add_argument("--spp", type=int, default=64)
@@ -168,10 +172,15 @@ def main():
             torch.cuda.synchronize()
 
     scene = scenes.get_scene(args.scene)
-    y0, y1 = hd.row_band(rank, world, args.height)
     pt = hippt.PathTracer()
     pt.setDevices([device])
-    pt.setRowRange(y0, y1)
+    if args.split == "interleave":
+        my_rows = hd.interleaved_rows(rank, world, args.height)
+        pt.setRowInterleave(rank, world)
+    else:
+        y0, y1 = hd.row_band(rank, world, args.height)
+        my_rows = np.arange(y0, y1)
+        pt.setRowRange(y0, y1)
     if args.wave_threshold is not None:
         pt.setOption(hippt.OPT_WAVE_THRESHOLD, args.wave_threshold)
     if args.chunk is not None:
@@ -220,8 +229,9 @@ def main():
     value = segments / elapsed_max / 1e6
 
     # output image of the last step: gathered bands (untimed), checksum on rank 0
-    px, _ = pt.readback(y0, y1)
-    full = hd.gather_bands(px, args.height, dist)
+    px = pt.readback()[0][my_rows]
+    full = (hd.gather_interleaved(px, args.height, dist) if args.split == "interleave"
+            else hd.gather_bands(px, args.height, dist))
 
     # roofline of the dominant (mesh) kernel, from this rank's counted pass and live events
     launches = max(1, st["traceLaunches"] // max(1, args.steps))
@@ -259,7 +269,8 @@ def main():
                 and args.height == 1080 and args.spp == 64 and args.depth == 8 else workload,
                 "scene": args.scene, "triangles": scene.num_tris, "spheres": scene.num_spheres,
                 "path_mode": args.path_mode, "width": args.width, "height": args.height,
-                "spp": args.spp, "max_depth": args.depth, "parallelism": f"row-bands x{world}",
+                "spp": args.spp, "max_depth": args.depth,
+                "parallelism": f"{'interleaved-rows' if args.split == 'interleave' else 'row-bands'} x{world}",
                 "segments_per_step": segments // max(1, args.steps),
                 "pixel_samples_per_step": samples // max(1, args.steps),
                 "mpixel_samples_per_s": round(samples / elapsed_max / 1e6, 3),

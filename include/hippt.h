@@ -123,6 +123,11 @@ bool hipptSetDevices(const int *deviceIds, int numDevices, const char **errorMes
 /* Restrict this process to rows [y0, y1) of the image (one-process-per-GPU launch);
  * y1 <= 0 means "to the last row".  Takes effect at the next Init. */
 bool hipptSetRowRange(int y0, int y1, const char **errorMessage);
+/* Alternative: this process renders rows phase, phase+stride, phase+2*stride, ... (one process
+ * per GPU with phase = rank, stride = world size balances the load: row bands of a scene differ
+ * by up to 1.6x in cost).  Clears a row range; hipptSetRowRange clears the interleave.  Takes
+ * effect at the next Init.  The image is bit-identical for any split. */
+bool hipptSetRowInterleave(int phase, int stride, const char **errorMessage);
 
 /* ---- rendering ------------------------------------------------------------------- */
 /* Renders `count` samples per pixel as frames firstFrame..firstFrame+count-1; the
@@ -180,7 +185,11 @@ enum {
     HIPPT_OPT_BLOCKS_PER_CU = 5,    /* persistent-grid residency (0 = occupancy query) */
     HIPPT_OPT_LDS_SCENE = 6,        /* 1 (default): small scenes are copied into LDS per block */
     HIPPT_OPT_PATH_MODE = 8,        /* 0 (default): persistent megakernel; 1: wavefront kernels */
-    HIPPT_OPT_WAVEFRONT_SLOTS = 9   /* wavefront path-state slots per device (default 2^24) */
+    HIPPT_OPT_WAVEFRONT_SLOTS = 9,  /* wavefront path-state slots per device (default 2^24) */
+    HIPPT_OPT_BVH_LEAF = 10,        /* max primitives per BVH leaf, 1..15; applies at the next upload */
+    HIPPT_OPT_BVH_TRAVERSAL_COST = 11, /* SAH node-step cost in 1/100 primitive tests; next upload */
+    HIPPT_OPT_BVH_MAX_DEPTH = 12,   /* interior-level bound (LDS stack per lane), 1..32; next upload */
+    HIPPT_OPT_DEVICE_ROWS = 13      /* hipptSetDevices split: 1 (default) interleaved rows, 0 bands; next Init */
 };
 bool hipptSetOption(int key, long long value);
 long long hipptGetOption(int key);

@@ -41,7 +41,7 @@ int ceil_log2(long long v) {
 
 class Builder {
 public:
-    Builder(std::vector<Prim> &p, float pad) : prims_(p), pad_(pad) {}
+    Builder(std::vector<Prim> &p, float pad, const BvhParams &params) : prims_(p), pad_(pad), par_(params) {}
 
     // Returns the child code for prims [b, e): interior node index or leaf code.
     int32_t build(int b, int e, int level, Box &bounds) {
@@ -61,17 +61,17 @@ public:
         int mid = -1;
         if (n <= 1) {
             mid = -1;
-        } else if (level + 1 + ceil_log2((n + kMaxLeafTris - 1) / kMaxLeafTris) >= kStackDepth) {
+        } else if (level + 1 + ceil_log2((n + par_.maxLeaf - 1) / par_.maxLeaf) >= par_.maxDepth) {
             // depth guard: from here object-median halving bounds the remaining levels
-            mid = n <= kMaxLeafTris ? -1 : median_split(b, e, axis);
+            mid = n <= par_.maxLeaf ? -1 : median_split(b, e, axis);
         } else if (ext[axis] <= 0.0f) {
-            mid = n > kMaxLeafTris ? b + n / 2 : -1;  // coincident centroids: split by index
+            mid = n > par_.maxLeaf ? b + n / 2 : -1;  // coincident centroids: split by index
         } else {
             float best_cost;
             int best_bin;
             sah(b, e, axis, cb, best_cost, best_bin);
             const float leaf_cost = float(n);
-            if (n <= kMaxLeafTris && leaf_cost <= best_cost) {
+            if (n <= par_.maxLeaf && leaf_cost <= best_cost) {
                 mid = -1;
             } else {
                 const float lo = cb.lo[axis], scale = kBins / ext[axis];
@@ -156,8 +156,8 @@ private:
             left.grow(bins[i]);
             lcnt += counts[i];
             if (lcnt == 0 || right_count[i + 1] == 0) continue;
-            // traversal cost 1, triangle test cost 1 (relative)
-            float cost = 1.0f + (left.area() * lcnt + right_area[i + 1] * right_count[i + 1]) / pa;
+            // one traversal step = traversalCost primitive tests
+            float cost = par_.traversalCost + (left.area() * lcnt + right_area[i + 1] * right_count[i + 1]) / pa;
             if (cost < best_cost) {
                 best_cost = cost;
                 best_bin = i;
@@ -167,11 +167,18 @@ private:
 
     std::vector<Prim> &prims_;
     float pad_;
+    BvhParams par_;
 };
 
 }  // namespace
 
-bool build_bvh_boxes(const float *boxes, int numPrims, float extentHint, Bvh &out, std::string &err) {
+bool build_bvh_boxes(const float *boxes, int numPrims, float extentHint, Bvh &out, std::string &err,
+                     const BvhParams &params) {
+    if (params.maxLeaf < 1 || params.maxLeaf > 15 || !(params.traversalCost > 0.0f) || params.maxDepth < 1 ||
+        params.maxDepth > kStackDepth) {
+        err = "invalid BVH build parameters";
+        return false;
+    }
     if (numPrims <= 0) {
         // RayTracer.h:398-400: a BVH over an empty range is an error.
         err = "BVH requires at least one primitive";
@@ -199,7 +206,7 @@ bool build_bvh_boxes(const float *boxes, int numPrims, float extentHint, Bvh &ou
         p.id = i;
     }
     const float pad = std::max(maxabs, 1e-3f) * (1.0f / 65536.0f);
-    Builder bld(prims, pad);
+    Builder bld(prims, pad, params);
     Box rootBox;
     // Node 0 must be interior: reserve it, then build the children.
     int32_t code = bld.build(0, numPrims, 0, rootBox);
@@ -214,8 +221,8 @@ bool build_bvh_boxes(const float *boxes, int numPrims, float extentHint, Bvh &ou
     out.leaves = bld.leaves;
     out.order.resize(size_t(numPrims));
     for (int i = 0; i < numPrims; ++i) out.order[size_t(i)] = prims[size_t(i)].id;
-    if (out.levels > kStackDepth) {
-        err = "BVH deeper than the kernel stack";
+    if (out.levels > params.maxDepth) {
+        err = "BVH deeper than the depth bound (too few levels for the primitives at this leaf size)";
         return false;
     }
     return true;

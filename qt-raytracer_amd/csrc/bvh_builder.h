@@ -18,6 +18,16 @@ constexpr int kStackDepth = 32;
 constexpr int kMaxLeafTris = 4;
 constexpr int kNodeWords = 16;  // 64 B: two child boxes + two child codes
 
+// Build parameters: SAH with a traversal step costing `traversalCost` primitive tests, leaves of
+// at most `maxLeaf` (<= 15, the leaf code's count field) primitives.
+// maxDepth bounds the interior levels (= the kernel's LDS stack entries per lane, so it sets
+// the occupancy of deep scenes); below the bound the split is SAH, near it object median.
+struct BvhParams {
+    int maxLeaf = kMaxLeafTris;
+    float traversalCost = 1.0f;
+    int maxDepth = kStackDepth;
+};
+
 struct Bvh {
     std::vector<uint32_t> nodes;  // kNodeWords per interior node; node 0 is the root
     std::vector<int> order;       // leaf order -> original primitive index
@@ -31,7 +41,8 @@ struct Bvh {
 bool build_bvh(const float *verts, int numTris, float extentHint, Bvh &out, std::string &err);
 // General primitives: boxes = numPrims * 6 floats (lo xyz, hi xyz); `order` maps leaf order
 // to the primitive index.
-bool build_bvh_boxes(const float *boxes, int numPrims, float extentHint, Bvh &out, std::string &err);
+bool build_bvh_boxes(const float *boxes, int numPrims, float extentHint, Bvh &out, std::string &err,
+                     const BvhParams &params = BvhParams());
 
 inline int32_t leaf_code(int first, int count) { return ~((first << 4) | count); }
 

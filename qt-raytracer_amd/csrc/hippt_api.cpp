@@ -36,13 +36,15 @@ using hippt::CameraF;
 
 constexpr int kStatWords = 32;  // [0..3] hipptStats counters, [4..19] phase profile
 
+constexpr size_t kQueueBytes = 8 * 32 * sizeof(unsigned);  // hippt_trace.h kQueues x kQueueStride
+
 struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
 };
 
 struct Ctx {
     int device = 0;
-    int y0 = 0, y1 = 0;  // image rows of this band
+    int y0 = 0, rows = 0, stride = 1;  // image rows y0, y0+stride, ... (rows of them)
     hipStream_t stream = nullptr;
     float4 *accum = nullptr;
     uint32_t *out = nullptr;
@@ -85,7 +87,9 @@ struct State {
     std::mutex mu;
     bool ready = false;
     int width = 0, height = 0;
-    int rowY0 = 0, rowY1 = 0;
+    int rowY0 = 0, rowY1 = 0;              // process rows: range [rowY0, rowY1) ...
+    int rowPhase = 0, rowStride = 1;       // ... or every rowStride-th row from rowPhase
+    bool deviceInterleave = true;          // devices of this process: interleaved rows (else bands)
     std::vector<int> devices;
     std::vector<Ctx> ctxs;
     unsigned *host = nullptr;  // pinned W*H ARGB frame (library-owned, as gState.hostOutput)
@@ -110,6 +114,7 @@ struct State {
     bool ldsScene = true;
     int pathMode = 0;             // 0 megakernel, 1 wavefront
     unsigned wfSlots = 1u << 24;  // wavefront path-state slots per device
+    hippt::BvhParams bvh;         // applied at the next scene upload
     // host-side timing accumulators
     double traceMs = 0, combineMs = 0;
     int traceLaunches = 0, combineLaunches = 0;
@@ -306,22 +311,38 @@ bool init_inner(int width, int height, const char **err) {
         HIP_TRY(hipGetDevice(&d));
         devs.push_back(d);
     }
-    const int ry0 = std::clamp(s.rowY0, 0, height);
-    const int ry1 = s.rowY1 <= 0 ? height : std::clamp(s.rowY1, ry0, height);
-    const int rows = ry1 - ry0;
+    // this process's rows: first p0, count pn, stride ps
+    int p0, pn, ps;
+    if (s.rowStride > 1) {
+        p0 = std::min(s.rowPhase, height);
+        ps = s.rowStride;
+        pn = p0 < height ? (height - p0 + ps - 1) / ps : 0;
+    } else {
+        p0 = std::clamp(s.rowY0, 0, height);
+        pn = (s.rowY1 <= 0 ? height : std::clamp(s.rowY1, p0, height)) - p0;
+        ps = 1;
+    }
     const int n = int(devs.size());
     s.ctxs.resize(size_t(n));
     for (int k = 0; k < n; ++k) {
         Ctx &c = s.ctxs[size_t(k)];
         c.device = devs[size_t(k)];
-        c.y0 = ry0 + int((long long)rows * k / n);
-        c.y1 = ry0 + int((long long)rows * (k + 1) / n);
+        if (s.deviceInterleave && n > 1) {  // device k: every n-th of the process's rows
+            c.y0 = p0 + ps * k;
+            c.rows = pn > k ? (pn - k + n - 1) / n : 0;
+            c.stride = ps * n;
+        } else {  // device k: a contiguous run of the process's rows
+            const int a = int((long long)pn * k / n), b = int((long long)pn * (k + 1) / n);
+            c.y0 = p0 + ps * a;
+            c.rows = b - a;
+            c.stride = ps;
+        }
         HIP_TRY(hipSetDevice(c.device));
         HIP_TRY(hipStreamCreateWithFlags(&c.stream, hipStreamNonBlocking));
-        const size_t px = size_t(c.y1 - c.y0) * size_t(width);
+        const size_t px = size_t(c.rows) * size_t(width);
         HIP_TRY(hipMalloc(&c.accum, std::max<size_t>(16, px * sizeof(float4))));
         HIP_TRY(hipMalloc(&c.out, std::max<size_t>(16, px * sizeof(uint32_t))));
-        HIP_TRY(hipMalloc(&c.queue, 64));
+        HIP_TRY(hipMalloc(&c.queue, kQueueBytes));
         HIP_TRY(hipMalloc(&c.stats, kStatWords * sizeof(unsigned long long)));
         HIP_TRY(hipMemsetAsync(c.accum, 0, px * sizeof(float4), c.stream));
         HIP_TRY(hipMemsetAsync(c.out, 0, px * sizeof(uint32_t), c.stream));
@@ -432,6 +453,17 @@ CameraF current_camera() {
 }
 
 // Enqueues `count` frames on every context (no host wait).
+// Copies a context's compact rows (c.rows rows of W pixels of `bytes` each) to their image rows
+// c.y0, c.y0 + c.stride, ... of a full-frame host buffer, on the context's stream.
+bool copy_rows_async(Ctx &c, void *dstFrame, const void *src, size_t bytes, const char **err) {
+    State &s = S();
+    if (c.rows <= 0) return true;
+    const size_t row = size_t(s.width) * bytes;
+    char *dst = static_cast<char *>(dstFrame) + size_t(c.y0) * row;
+    HIP_TRY(hipMemcpy2DAsync(dst, row * size_t(c.stride), src, row, row, size_t(c.rows), hipMemcpyDeviceToHost, c.stream));
+    return true;
+}
+
 bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const char **err) {
     State &s = S();
     if (!s.ready) return fail(err, "HIP path tracer not initialized");
@@ -440,11 +472,12 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
     const CameraF cam = mesh ? current_camera() : CameraF{};
     for (Ctx &c : s.ctxs) {
         HIP_TRY(hipSetDevice(c.device));
-        const int rows = c.y1 - c.y0;
+        const int rows = c.rows;
         const unsigned bandPixels = unsigned(rows) * unsigned(s.width);
         if (rows > 0 && count > 0) {
             if (!mesh) {
-                hippt::Sphere4Params p{c.accum, c.out, c.stats, s.width, s.height, c.y0, rows, firstFrame, count, maxDepth};
+                hippt::Sphere4Params p{c.accum, c.out, c.stats, s.width, s.height, c.y0, rows, c.stride, firstFrame, count,
+                                       maxDepth};
                 EventPair ev;
                 if (!next_events(c, ev, err)) return false;
                 HIP_TRY(hipEventRecord(ev.a, c.stream));
@@ -504,6 +537,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.height = s.height;
                         p.y0 = c.y0;
                         p.bandRows = rows;
+                        p.rowStride = c.stride;
                         p.firstFrame = firstFrame + b;
                         p.frames = nf;
                         p.maxDepth = maxDepth;
@@ -524,7 +558,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                             long long blocks = (long long)c.cus * bpc;
                             blocks = std::min<long long>(blocks, (total + hippt::kMeshBlock - 1) / hippt::kMeshBlock);
                             blocks = std::max<long long>(blocks, 1);
-                            HIP_TRY(hipMemsetAsync(c.queue, 0, sizeof(unsigned), c.stream));
+                            HIP_TRY(hipMemsetAsync(c.queue, 0, kQueueBytes, c.stream));
                             EventPair ev;
                             if (!next_events(c, ev, err)) return false;
                             HIP_TRY(hipEventRecord(ev.a, c.stream));
@@ -544,8 +578,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
             }
         }
         if (copy && rows > 0) {
-            HIP_TRY(hipMemcpyAsync(s.host + size_t(c.y0) * size_t(s.width), c.out, size_t(bandPixels) * sizeof(uint32_t),
-                                   hipMemcpyDeviceToHost, c.stream));
+            if (!copy_rows_async(c, s.host, c.out, sizeof(uint32_t), err)) return false;
         }
     }
     return true;
@@ -668,7 +701,7 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
     for (int i = 0; i < 3; ++i) extent = std::max(extent, float(std::fabs(lookfrom[i])));
     hippt::Bvh bvh;
     std::string msg;
-    if (!hippt::build_bvh_boxes(boxes.data(), numPrims, extent, bvh, msg)) return fail(err, msg);
+    if (!hippt::build_bvh_boxes(boxes.data(), numPrims, extent, bvh, msg, s.bvh)) return fail(err, msg);
     SceneHost &sc = s.scene;
     sc.nodes.assign(bvh.nodes.size() / 4, float4{});
     std::memcpy(sc.nodes.data(), bvh.nodes.data(), bvh.nodes.size() * sizeof(uint32_t));
@@ -810,6 +843,18 @@ extern "C" bool hipptSetRowRange(int y0, int y1, const char **err) {
     if (y0 < 0 || (y1 > 0 && y1 < y0)) return fail(err, "invalid row range");
     S().rowY0 = y0;
     S().rowY1 = y1;
+    S().rowPhase = 0;
+    S().rowStride = 1;
+    return true;
+}
+
+extern "C" bool hipptSetRowInterleave(int phase, int stride, const char **err) {
+    std::lock_guard<std::mutex> g(S().mu);
+    if (stride < 1 || phase < 0 || phase >= stride) return fail(err, "invalid row interleave");
+    S().rowPhase = phase;
+    S().rowStride = stride;
+    S().rowY0 = 0;
+    S().rowY1 = 0;
     return true;
 }
 
@@ -841,10 +886,7 @@ extern "C" bool hipptRenderFramesPresent(int firstFrame, int count, int maxDepth
     for (Ctx &c : s.ctxs) {
         HIP_TRY(hipSetDevice(c.device));
         if (!c.presentEv[b]) HIP_TRY(hipEventCreateWithFlags(&c.presentEv[b], hipEventDisableTiming));
-        const size_t bandPixels = size_t(c.y1 - c.y0) * size_t(s.width);
-        if (bandPixels)
-            HIP_TRY(hipMemcpyAsync(s.present[b] + size_t(c.y0) * size_t(s.width), c.out, bandPixels * sizeof(uint32_t),
-                                   hipMemcpyDeviceToHost, c.stream));
+        if (!copy_rows_async(c, s.present[b], c.out, sizeof(uint32_t), err)) return false;
         HIP_TRY(hipEventRecord(c.presentEv[b], c.stream));
         if (!harvest_locked(c, err)) return false;
     }
@@ -889,12 +931,9 @@ extern "C" bool hipptReadback(unsigned int *pixels, float *accum, const char **e
     if (!sync_locked(err)) return false;
     for (Ctx &c : s.ctxs) {
         HIP_TRY(hipSetDevice(c.device));
-        const size_t px = size_t(c.y1 - c.y0) * size_t(s.width);
-        if (px == 0) continue;
-        if (pixels)
-            HIP_TRY(hipMemcpy(pixels + size_t(c.y0) * s.width, c.out, px * sizeof(uint32_t), hipMemcpyDeviceToHost));
-        if (accum)
-            HIP_TRY(hipMemcpy(accum + size_t(c.y0) * s.width * 4, c.accum, px * sizeof(float4), hipMemcpyDeviceToHost));
+        if (pixels && !copy_rows_async(c, pixels, c.out, sizeof(uint32_t), err)) return false;
+        if (accum && !copy_rows_async(c, accum, c.accum, sizeof(float4), err)) return false;
+        HIP_TRY(hipStreamSynchronize(c.stream));
     }
     return true;
 }
@@ -905,7 +944,7 @@ extern "C" bool hipptResetAccumulation(const char **err) {
     if (!s.ready) return fail(err, "HIP path tracer not initialized");
     for (Ctx &c : s.ctxs) {
         HIP_TRY(hipSetDevice(c.device));
-        const size_t px = size_t(c.y1 - c.y0) * size_t(s.width);
+        const size_t px = size_t(c.rows) * size_t(s.width);
         HIP_TRY(hipMemsetAsync(c.accum, 0, px * sizeof(float4), c.stream));
         HIP_TRY(hipStreamSynchronize(c.stream));
     }
@@ -1000,6 +1039,22 @@ extern "C" bool hipptSetOption(int key, long long value) {
         if (value < 64 || value > (1LL << 26)) return false;
         s.wfSlots = unsigned(value);
         return true;
+    case HIPPT_OPT_BVH_LEAF:
+        if (value < 1 || value > 15) return false;
+        s.bvh.maxLeaf = int(value);
+        return true;
+    case HIPPT_OPT_BVH_TRAVERSAL_COST:
+        if (value < 1 || value > 100000) return false;
+        s.bvh.traversalCost = float(value) / 100.0f;
+        return true;
+    case HIPPT_OPT_BVH_MAX_DEPTH:
+        if (value < 1 || value > hippt::kStackDepth) return false;
+        s.bvh.maxDepth = int(value);
+        return true;
+    case HIPPT_OPT_DEVICE_ROWS:
+        if (value < 0 || value > 1) return false;
+        s.deviceInterleave = value == 1;
+        return true;
     default: return false;
     }
 }
@@ -1016,6 +1071,10 @@ extern "C" long long hipptGetOption(int key) {
     case HIPPT_OPT_LDS_SCENE: return s.ldsScene ? 1 : 0;
     case HIPPT_OPT_PATH_MODE: return s.pathMode;
     case HIPPT_OPT_WAVEFRONT_SLOTS: return s.wfSlots;
+    case HIPPT_OPT_BVH_LEAF: return s.bvh.maxLeaf;
+    case HIPPT_OPT_BVH_TRAVERSAL_COST: return (long long)std::lround(s.bvh.traversalCost * 100.0f);
+    case HIPPT_OPT_BVH_MAX_DEPTH: return s.bvh.maxDepth;
+    case HIPPT_OPT_DEVICE_ROWS: return s.deviceInterleave ? 1 : 0;
     default: return -1;
     }
 }

@@ -14,17 +14,17 @@ struct CameraF {  // layout == hipptCamera (include/hippt.h)
     float reserved;
 };
 
-// Legacy 4-sphere scene (CudaPathTracerKernel.cu:136-179), rows [y0, y0+rows).
+// Legacy 4-sphere scene (CudaPathTracerKernel.cu:136-179).
 struct Sphere4Params {
     float4 *accum;      // rows*width RGBA
     uint32_t *out;      // rows*width ARGB
     unsigned long long *stats;
-    int width, height, y0, rows;
+    int width, height, y0, rows, rowStride;  // image rows y0 + k*rowStride, k < rows
     int firstFrame, frames, maxDepth;
 };
 
-// Triangle-mesh megakernel: one persistent grid drains `totalItems` (pixel, frame)
-// samples of rows [y0, y0+bandRows) and frames [firstFrame, firstFrame+frames).
+// Mesh megakernel: one persistent grid drains `totalItems` (pixel, frame) samples of the band's
+// rows and frames [firstFrame, firstFrame+frames).
 struct MeshParams {
     const float4 *nodes;   // 4 float4 per interior node (bvh_builder.h layout)
     // 3 float4 per primitive, BVH leaf order, tag = third .z (int bits):
@@ -36,11 +36,11 @@ struct MeshParams {
     const float4 *shade;
     const float4 *mats;    // 2 float4 per material: (albedo rgb, kind) (fuzz, ir, -, -)
     float *scratch;        // 3 planes (R, G, B) of totalItems floats: per-sample radiance
-    unsigned *queue;       // global work counter (zeroed before launch)
+    unsigned *queue;       // kQueues work counters, 128 B apart (zeroed before launch)
     unsigned long long *stats;  // [0] segments, [1] pixel samples, [2] node visits, [3] tri tests
     CameraF cam;
     float invW, invH;      // 1/max(1,W-1), 1/max(1,H-1) (RayTracerFboItem.cpp:61-64)
-    int width, height, y0, bandRows;
+    int width, height, y0, bandRows, rowStride;  // band row k is image row y0 + k*rowStride
     int firstFrame, frames, maxDepth;
     unsigned bandPixels, totalItems;
     float rcpBandPixels, rcpWidth;  // 1/bandPixels, 1/width for the item -> (frame, x, y) split

@@ -20,6 +20,8 @@
 // Arithmetic contract: see hippt_trace.h (shared with oracle/pt_oracle.c).
 #include "hippt_trace.h"
 
+#include <algorithm>
+
 #pragma clang fp contract(off)
 
 namespace hippt {
@@ -87,7 +89,7 @@ __global__ __launch_bounds__(256) void sphere4_kernel(Sphere4Params P) {
     if (idx < P.rows * P.width) {
         const int yb = idx / P.width;
         const int x = idx - yb * P.width;
-        const int y = P.y0 + yb;
+        const int y = P.y0 + yb * P.rowStride;
         float4 acc = P.accum[idx];
         uint32_t outp = 0;
         const float wd = float(max(1, P.width - 1));
@@ -161,8 +163,34 @@ __global__ __launch_bounds__(256) void sphere4_kernel(Sphere4Params P) {
 // conflict), primitives at 48 bytes (12 dwords, likewise), shading records at 16 bytes.
 constexpr int kLdsNodeF4 = 5;
 
+#ifdef HIPPT_DEBUG_TIMELINE
+// per wave: [0] start, [1] first drained fetch, [2] end (s_memrealtime, 100 MHz), [3] items,
+// [4] HW_ID, [5] XCC_ID
+__device__ unsigned long long g_timeline[65536 * 6];
+#endif
+
+// SGPR budget.  A wave's SGPR allocation (granule 16) plus the 16 the trap handler reserves
+// must fit 7 waves in a SIMD's 800 SGPRs: <= 96.  Unbounded, the compiler used 97-100, the
+// hardware then held 6 blocks per CU while the occupancy query (which does not count the trap
+// reservation) reported 7 — 1/7 of the persistent grid started only when others finished
+// (per-wave timeline, tools/timeline.py) and ran as a tail.  At 96: all blocks resident,
+// Cornell +0.5%, blob +1.3%.
+#ifndef HIPPT_NUM_SGPR
+#define HIPPT_NUM_SGPR 96
+#endif
+#define HIPPT_SGPR_ATTR __attribute__((amdgpu_num_sgpr(HIPPT_NUM_SGPR)))
+
 template <bool STATS, bool LDS_SCENE, bool FULL>
-__global__ __launch_bounds__(kMeshBlock, HIPPT_MESH_WAVES_PER_EU) void mesh_kernel(MeshParams P) {
+__global__ __launch_bounds__(kMeshBlock, HIPPT_MESH_WAVES_PER_EU) HIPPT_SGPR_ATTR void mesh_kernel(MeshParams P) {
+#ifdef HIPPT_DEBUG_TIMELINE
+    const unsigned tlw = blockIdx.x * 4u + (threadIdx.x >> 6);
+    unsigned long long tlDrained = 0, tlItems = 0;
+    if (__lane_id() == 0 && tlw < 65536) {
+        g_timeline[6 * tlw] = __builtin_amdgcn_s_memrealtime();
+        g_timeline[6 * tlw + 4] = __builtin_amdgcn_s_getreg(0xF804);  // HW_REG_HW_ID
+        g_timeline[6 * tlw + 5] = __builtin_amdgcn_s_getreg(0xF814);  // HW_REG_XCC_ID
+    }
+#endif
     // Per-lane traversal stack, P.stackDepth (= BVH interior levels) entries per lane, sized
     // at launch so shallow BVHs do not cap occupancy.  Entry k of lane t at stk[k*256 + t]:
     // a wave's lanes hit 64 consecutive dwords, conflict-free for any mix of depths.
@@ -185,7 +213,8 @@ __global__ __launch_bounds__(kMeshBlock, HIPPT_MESH_WAVES_PER_EU) void mesh_kern
     }
     constexpr int nodeF4 = LDS_SCENE ? kLdsNodeF4 : 4;
 
-    unsigned poolNext = 0, poolEnd = 0;
+    WorkQueue Q;
+    queue_begin(Q, P.totalItems, P.chunk);
     unsigned item = kNone;
     uint32_t rng = 0;
     int depth = 0;
@@ -206,7 +235,11 @@ __global__ __launch_bounds__(kMeshBlock, HIPPT_MESH_WAVES_PER_EU) void mesh_kern
         prof<STATS>(pc, 0);
         // ---- refill: every lane whose sample ended takes the next (pixel, frame) -------------
         if (__ballot(need)) {
-            const unsigned it = wave_fetch(need, poolNext, poolEnd, P.queue, P.chunk, P.totalItems);
+            const unsigned it = queue_fetch(need, Q, P.queue, P.totalItems, P.chunk);
+#ifdef HIPPT_DEBUG_TIMELINE
+            if (!tlDrained && __ballot(need && it == kNone)) tlDrained = __builtin_amdgcn_s_memrealtime();
+            tlItems += __popcll(__ballot(it != kNone));
+#endif
             if (need) {
                 need = false;
                 item = it;
@@ -256,6 +289,13 @@ __global__ __launch_bounds__(kMeshBlock, HIPPT_MESH_WAVES_PER_EU) void mesh_kern
         }
     }
 
+#ifdef HIPPT_DEBUG_TIMELINE
+    if (__lane_id() == 0 && tlw < 65536) {
+        g_timeline[6 * tlw + 1] = tlDrained;
+        g_timeline[6 * tlw + 2] = __builtin_amdgcn_s_memrealtime();
+        g_timeline[6 * tlw + 3] = tlItems;
+    }
+#endif
     segs = wave_sum(segs);
     samples = wave_sum(samples);
     if (STATS) {
@@ -300,6 +340,15 @@ __global__ __launch_bounds__(256) void combine_kernel(CombineParams P) {
 
 }  // namespace
 
+#ifdef HIPPT_DEBUG_TIMELINE
+extern "C" int hipptDebugTimeline(unsigned long long *out, int maxWaves) {
+    const int n = maxWaves < 65536 ? maxWaves : 65536;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_timeline), size_t(n) * 6 * sizeof(unsigned long long)) == hipSuccess
+               ? n
+               : -1;
+}
+#endif
+
 hipError_t launch_sphere4(const Sphere4Params &p, hipStream_t s) {
     const long long n = (long long)p.rows * p.width;
     if (n <= 0) return hipSuccess;
@@ -316,6 +365,8 @@ size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris) {
 }
 
 size_t mesh_lds_scene_limit() { return 24u << 10; }
+
+static constexpr int kMaxResidentBlocks = 7;
 
 using MeshFn = void (*)(MeshParams);
 static MeshFn mesh_fn(bool count, bool lds, bool full) {
@@ -350,7 +401,10 @@ int mesh_blocks_per_cu(bool countTraversal, bool full, int stackDepth, int ldsNo
     hipError_t e =
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mesh_fn(countTraversal, lds, full), kMeshBlock, bytes);
     if (e != hipSuccess || n <= 0) n = 1;
-    return n;
+    // the query ignores the trap handler's SGPRs: with HIPPT_NUM_SGPR (<= 96) a SIMD holds at
+    // most 7 waves, i.e. 7 blocks of 4 waves per CU; a larger persistent grid leaves blocks
+    // waiting for a slot until others finish
+    return std::min(n, kMaxResidentBlocks);
 }
 
 }  // namespace hippt

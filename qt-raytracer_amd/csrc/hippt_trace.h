@@ -88,6 +88,78 @@ __device__ __forceinline__ unsigned wave_fetch(bool req, unsigned &poolNext, uns
     return (req && item < total) ? item : kNone;
 }
 
+// Work distribution of the persistent megakernel over items [0, total).  The items are split
+// into kQueues contiguous queues, one per XCD (block b is dispatched to XCD b % 8), each with
+// its counter on its own 128-byte line (queue[g * kQueueStride]).  A wave's first chunk is
+// assigned statically (no atomic at kernel start, where all waves would contend), further
+// chunks come from its home queue's counter, chunks shrink to kTailChunk items once the queue
+// is within one chunk per wave of its end (a short tail), and a wave whose home queue is
+// drained moves on to the others.  Counters start at 0 and count dynamically claimed items.
+constexpr unsigned kQueues = 8, kQueueStride = 32, kTailChunk = 64;
+
+struct WorkQueue {
+    unsigned g, left;  // current queue, queues not yet found drained
+    unsigned next, end;  // this wave's pool [next, end) (all items of queue g)
+    unsigned qEnd, dynBase, waves;  // queue g: end, first dynamically claimed item, home waves
+};
+
+__device__ __forceinline__ unsigned queue_start(unsigned total, unsigned g) {
+    return unsigned((unsigned long long)total * g / kQueues);
+}
+
+__device__ __forceinline__ void queue_select(WorkQueue &Q, unsigned g, unsigned total, unsigned chunk) {
+    Q.g = g;
+    Q.qEnd = queue_start(total, g + 1);
+    Q.waves = 4u * ((gridDim.x + kQueues - 1 - g) / kQueues);  // blocks b = g mod 8, 4 waves each
+    Q.dynBase = queue_start(total, g) + Q.waves * chunk;
+}
+
+__device__ __forceinline__ void queue_begin(WorkQueue &Q, unsigned total, unsigned chunk) {
+    queue_select(Q, blockIdx.x % kQueues, total, chunk);
+    Q.left = kQueues;
+    const unsigned wid = (blockIdx.x / kQueues) * 4u + (threadIdx.x >> 6);
+    Q.next = min(queue_start(total, Q.g) + wid * chunk, Q.qEnd);
+    Q.end = min(Q.next + chunk, Q.qEnd);
+}
+
+// One item per requesting lane (kNone once every queue is drained).  Whole wave, uniform
+// control flow; the pool and queue state are wave-uniform.
+__device__ __forceinline__ unsigned queue_fetch(bool req, WorkQueue &Q, unsigned *ctr, unsigned total,
+                                                unsigned chunk) {
+    unsigned item = kNone;
+    bool want = req;
+    unsigned long long m = __ballot(want);
+    unsigned rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
+    unsigned avail = Q.end - Q.next;
+    if (want && rank < avail) {
+        item = Q.next + rank;
+        want = false;
+    }
+    Q.next += min(unsigned(__popcll(m)), avail);
+    while (Q.left && __ballot(want)) {
+        m = __ballot(want);
+        rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
+        const unsigned c = Q.qEnd - min(Q.end, Q.qEnd) < Q.waves * chunk ? kTailChunk : chunk;
+        unsigned base = 0;
+        if (__lane_id() == 0) base = atomicAdd(&ctr[Q.g * kQueueStride], c);
+        base = __builtin_amdgcn_readfirstlane(base) + Q.dynBase;
+        if (base < Q.qEnd) {
+            Q.next = base;
+            Q.end = min(base + c, Q.qEnd);
+            avail = Q.end - Q.next;
+            if (want && rank < avail) {
+                item = Q.next + rank;
+                want = false;
+            }
+            Q.next += min(unsigned(__popcll(m)), avail);
+        } else if (--Q.left) {
+            queue_select(Q, Q.g + 1 == kQueues ? 0u : Q.g + 1, total, chunk);
+            Q.next = Q.end = 0;
+        }
+    }
+    return item;
+}
+
 // Wave-aggregated append of one entry per requesting lane to queue[] (one atomic per wave).
 __device__ __forceinline__ void wave_append(bool req, unsigned value, unsigned *queue, unsigned *count) {
     const unsigned long long mask = __ballot(req);
@@ -136,7 +208,7 @@ __device__ __forceinline__ void camera_sample(const MeshParams &P, unsigned it, 
     unsigned fl, p, yb, x;
     divmod(it, P.bandPixels, P.rcpBandPixels, fl, p);
     divmod(p, unsigned(P.width), P.rcpWidth, yb, x);
-    const unsigned y = unsigned(P.y0) + yb;
+    const unsigned y = unsigned(P.y0) + yb * unsigned(P.rowStride);
     rng = pixel_seed(x, y, unsigned(P.width), unsigned(P.firstFrame) + fl);
     const float s = (float(x) + rand01(rng)) * P.invW;
     const float t = (float(y) + rand01(rng)) * P.invH;

@@ -34,6 +34,10 @@ OPT_BLOCKS_PER_CU = 5
 OPT_LDS_SCENE = 6
 OPT_PATH_MODE = 8
 OPT_WAVEFRONT_SLOTS = 9
+OPT_BVH_LEAF = 10
+OPT_BVH_TRAVERSAL_COST = 11
+OPT_BVH_MAX_DEPTH = 12
+OPT_DEVICE_ROWS = 13
 
 # Every symbol include/hippt.h declares (checked by tests/test_abi_cpu.py).
 EXPORTS = (
@@ -41,7 +45,7 @@ EXPORTS = (
     "hipPathTracerInit", "hipPathTracerRender", "hipPathTracerShutdown",
     "hipptBuildCamera", "hipptUseBuiltinScene", "hipptUploadMesh", "hipptUploadScene", "hipptReadMesh",
     "hipptFreeMesh", "hipptSetCamera",
-    "hipptDeviceCount", "hipptSetDevices", "hipptSetRowRange",
+    "hipptDeviceCount", "hipptSetDevices", "hipptSetRowRange", "hipptSetRowInterleave",
     "hipptRenderFrames", "hipptRenderFramesAsync", "hipptSynchronize", "hipptRenderFramesPresent",
     "hipptLatestFrame", "hipptReadback",
     "hipptResetAccumulation", "hipptGetStats", "hipptResetStats", "hipptGetCounters", "hipptSetOption",
@@ -127,6 +131,7 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     sig("hipptDeviceCount", c_int)
     sig("hipptSetDevices", c_bool, p_int, c_int, pp_char)
     sig("hipptSetRowRange", c_bool, c_int, c_int, pp_char)
+    sig("hipptSetRowInterleave", c_bool, c_int, c_int, pp_char)
     sig("hipptRenderFrames", c_bool, c_int, c_int, c_int, pp_uint, pp_char)
     sig("hipptRenderFramesAsync", c_bool, c_int, c_int, c_int, pp_char)
     sig("hipptSynchronize", c_bool, pp_char)
@@ -375,6 +380,12 @@ class PathTracer:
         e = ctypes.c_char_p()
         if not self._lib.hipptSetRowRange(int(y0), int(y1), ctypes.byref(e)):
             raise HipptError(_err(e, "bad row range"))
+
+    def setRowInterleave(self, phase: int, stride: int) -> None:  # noqa: N802
+        """Render rows phase, phase+stride, ... (one process per GPU: phase=rank, stride=world)."""
+        e = ctypes.c_char_p()
+        if not self._lib.hipptSetRowInterleave(int(phase), int(stride), ctypes.byref(e)):
+            raise HipptError(_err(e, "bad row interleave"))
 
     def setOption(self, key: int, value: int) -> None:  # noqa: N802
         if not self._lib.hipptSetOption(int(key), int(value)):

@@ -1,9 +1,11 @@
-"""One-process-per-GPU row banding.
+"""One-process-per-GPU row split.
 
 Pixels are independent and the RNG seed depends only on the global (x, y, frame), so each
-rank renders its contiguous band of rows with no data-path collective; the image is the
-concatenation of the bands.  The only exchange is the (untimed) host gather of the ARGB
-bands for output, and the max-over-ranks of the timed interval.
+rank renders its own rows with no data-path collective.  Two splits: contiguous row bands
+(row_band) and interleaved rows (rank r renders rows r, r+N, r+2N, ...: interleaved_rows).
+Bands of a scene differ in cost by up to 1.6x (sky vs. walls), so the N-GPU step time — the
+slowest rank — favours interleaving.  The only exchanges are the (untimed) host gather of the
+ARGB rows for output and the max-over-ranks of the timed interval.
 """
 from __future__ import annotations
 
@@ -15,6 +17,13 @@ def row_band(rank: int, world: int, height: int):
     if world <= 0 or not 0 <= rank < world:
         raise ValueError(f"bad rank {rank} of {world}")
     return (rank * height) // world, ((rank + 1) * height) // world
+
+
+def interleaved_rows(rank: int, world: int, height: int) -> np.ndarray:
+    """Rows rank, rank+N, ... < H — libhippt's hipptSetRowInterleave(rank, N)."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} of {world}")
+    return np.arange(rank, height, world)
 
 
 def env_rank():
@@ -64,3 +73,23 @@ def gather_bands(band: np.ndarray, height: int, dist=None) -> np.ndarray:
         full[y0:y1] = outs[r].numpy()[: y1 - y0]
     del rank
     return full.view(band.dtype).reshape((height,) + width_shape)
+
+
+def gather_interleaved(rows: np.ndarray, height: int, dist=None) -> np.ndarray:
+    """Full-height images from per-rank interleaved rows (rows: (len(interleaved_rows), W, ...))."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return rows
+    import torch
+    world = dist.get_world_size()
+    width_shape = rows.shape[1:]
+    row_bytes = int(np.prod(width_shape, dtype=np.int64)) * rows.dtype.itemsize
+    max_rows = -(-height // world)
+    buf = np.zeros((max_rows, row_bytes), np.uint8)
+    buf[: rows.shape[0]] = np.ascontiguousarray(rows).view(np.uint8).reshape(rows.shape[0], row_bytes)
+    outs = [torch.zeros((max_rows, row_bytes), dtype=torch.uint8) for _ in range(world)]
+    dist.all_gather(outs, torch.from_numpy(buf))
+    full = np.zeros((height, row_bytes), np.uint8)
+    for r in range(world):
+        idx = interleaved_rows(r, world, height)
+        full[idx] = outs[r].numpy()[: len(idx)]
+    return full.view(rows.dtype).reshape((height,) + width_shape)

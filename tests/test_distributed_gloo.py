@@ -1,6 +1,6 @@
-"""Multi-process row banding on CPU (gloo, world_size 2): the host logic bench.py uses for
-N GPUs — band split, max/sum over ranks, and the host gather of ARGB bands — with the CPU
-oracle standing in for each rank's GPU render (test infrastructure only)."""
+"""Multi-process row splits on CPU (gloo, world_size 2 and 3): the host logic bench.py uses for
+N GPUs — interleaved rows or bands, max/sum over ranks, and the host gather of ARGB rows — with
+the CPU oracle standing in for each rank's GPU render (test infrastructure only)."""
 import os
 import socket
 
@@ -23,16 +23,25 @@ def _free_port():
     return port
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, split="bands"):
     import pyoracle as po
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        y0, y1 = hd.row_band(rank, world, H)
         ms = po.MeshScene(scenes.cornell34(), W, H)
-        px, acc, segs, samples = ms.frames(0, SPP, DEPTH, y0=y0, y1=y1, nthreads=1)
-        full_px = hd.gather_bands(px, H, dist)
-        full_acc = hd.gather_bands(acc, H, dist)
+        if split == "bands":
+            y0, y1 = hd.row_band(rank, world, H)
+            px, acc, segs, samples = ms.frames(0, SPP, DEPTH, y0=y0, y1=y1, nthreads=1)
+            full_px = hd.gather_bands(px, H, dist)
+            full_acc = hd.gather_bands(acc, H, dist)
+        else:  # interleaved rows rank, rank+N, ...: one oracle row at a time
+            parts = [ms.frames(0, SPP, DEPTH, y0=int(y), y1=int(y) + 1, nthreads=1)
+                     for y in hd.interleaved_rows(rank, world, H)]
+            px = np.concatenate([p[0] for p in parts])
+            acc = np.concatenate([p[1] for p in parts])
+            segs = sum(p[2] for p in parts)
+            full_px = hd.gather_interleaved(px, H, dist)
+            full_acc = hd.gather_interleaved(acc, H, dist)
         total_segs = hd.sum_over_ranks(segs, dist)
         slowest = hd.max_over_ranks(float(rank + 1), dist)
         if rank == 0:
@@ -43,10 +52,10 @@ def _worker(rank, world, port, out_dir):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_row_bands_gather_to_single_process_image(tmp_path, world):
+@pytest.mark.parametrize("world,split", [(2, "bands"), (3, "bands"), (2, "interleave"), (3, "interleave")])
+def test_row_split_gathers_to_single_process_image(tmp_path, world, split):
     import pyoracle as po
-    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True,
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), split), nprocs=world, join=True,
                        start_method="spawn")
     px = np.load(tmp_path / "px.npy")
     acc = np.load(tmp_path / "acc.npy")
@@ -66,6 +75,13 @@ def test_row_band_partition_covers_image():
             assert all(bands[i][1] == bands[i + 1][0] for i in range(world - 1))
     with pytest.raises(ValueError):
         hd.row_band(2, 2, 10)
+
+
+def test_interleaved_rows_partition_image():
+    for world in (1, 2, 3, 8):
+        for h in (1, 7, 1080):
+            rows = np.concatenate([hd.interleaved_rows(r, world, h) for r in range(world)])
+            assert np.array_equal(np.sort(rows), np.arange(h))
 
 
 def test_gather_without_process_group_is_identity():

@@ -21,6 +21,7 @@ def pt():
     t = hippt.PathTracer()
     t.setDevices([])
     t.setRowRange(0, 0)
+    t.setOption(hippt.OPT_DEVICE_ROWS, 1)
     t.useBuiltinScene(hippt.SCENE_SPHERE4)
     for k, v in ((hippt.OPT_WAVE_THRESHOLD, 32), (hippt.OPT_SCRATCH_MB, 4096), (hippt.OPT_CHUNK, 256),
                  (hippt.OPT_COUNT_TRAVERSAL, 0), (hippt.OPT_BLOCKS_PER_CU, 0), (hippt.OPT_LDS_SCENE, 1),
@@ -256,6 +257,47 @@ def test_mesh_row_range_and_two_contexts(pt):
     two = pt.readback()
     _assert_same(two[0], two[1], full[0], full[1])
     assert np.array_equal(pt.hostPixels(), full[0])
+
+
+@pytest.mark.parametrize("device_rows", [0, 1])
+def test_row_interleave_and_device_split(pt, device_rows):
+    """Interleaved rows (one process per GPU: rank r renders rows r, r+N, ...) and both in-process
+    device splits give the single-context image bit for bit."""
+    sc = scenes.cornell34()
+    pt.uploadMesh(sc)
+    w, h = 48, 37
+    assert pt.initialize(w, h)
+    assert pt.renderFrames(3, 8)
+    full = pt.readback()
+    for phase, stride in ((0, 3), (2, 3), (1, 8)):
+        pt.setRowInterleave(phase, stride)
+        assert pt.initialize(w, h)
+        assert pt.renderFrames(3, 8)
+        got = pt.readback()
+        rows = np.arange(phase, h, stride)
+        _assert_same(got[0][rows], got[1][rows], full[0][rows], full[1][rows])
+        other = np.setdiff1d(np.arange(h), rows)
+        assert not got[0][other].any()
+    pt.setRowRange(0, 0)
+    pt.setOption(hippt.OPT_DEVICE_ROWS, device_rows)
+    pt.setDevices([0, 0, 0])
+    assert pt.initialize(w, h)
+    assert pt.renderFrames(3, 8)
+    three = pt.readback()
+    _assert_same(three[0], three[1], full[0], full[1])
+    assert np.array_equal(pt.hostPixels(), full[0])
+    pt.setOption(hippt.OPT_DEVICE_ROWS, 1)
+
+
+def test_legacy_scene_row_interleave(pt):
+    assert pt.initialize(40, 23)
+    assert pt.renderFrames(2, 6)
+    full = pt.readback()
+    pt.setRowInterleave(1, 4)
+    assert pt.initialize(40, 23)
+    assert pt.renderFrames(2, 6)
+    got = pt.readback()
+    _assert_same(got[0][1::4], got[1][1::4], full[0][1::4], full[1][1::4])
 
 
 def test_single_triangle_and_degenerate_sizes(pt):

@@ -2,7 +2,8 @@
 """Option sweep in one process (GPU box): Msamples/s per libhippt option setting.
 
 usage: python tools/sweep.py [--scene cornell34] [--steps 3] KEY=v1,v2 [KEY=...]
-keys: wave (HIPPT_OPT_WAVE_THRESHOLD), chunk, scratch (MB), bpc (blocks per CU)
+keys: wave (HIPPT_OPT_WAVE_THRESHOLD), chunk, scratch (MB), bpc (blocks per CU), lds, mode, slots,
+      leaf (max primitives per BVH leaf), tcost (SAH traversal cost x100)
 Each combination: one warmup step, then `steps` timed steps; prints one JSON line each.
 """
 from __future__ import annotations
@@ -22,7 +23,9 @@ from hippt import scenes  # noqa: E402
 
 KEYS = {"wave": hippt.OPT_WAVE_THRESHOLD, "chunk": hippt.OPT_CHUNK, "scratch": hippt.OPT_SCRATCH_MB,
         "bpc": hippt.OPT_BLOCKS_PER_CU, "lds": hippt.OPT_LDS_SCENE, "mode": hippt.OPT_PATH_MODE,
-        "slots": hippt.OPT_WAVEFRONT_SLOTS}
+        "slots": hippt.OPT_WAVEFRONT_SLOTS, "leaf": hippt.OPT_BVH_LEAF, "tcost": hippt.OPT_BVH_TRAVERSAL_COST,
+        "depth": hippt.OPT_BVH_MAX_DEPTH}
+REUPLOAD = {"leaf", "tcost", "depth"}  # build parameters: take effect at the next upload
 
 
 def main():
@@ -46,6 +49,8 @@ def main():
     for combo in itertools.product(*axes) if axes else [()]:
         for k, v in combo:
             pt.setOption(KEYS[k], v)
+        if any(k in REUPLOAD for k, _ in combo):
+            pt.uploadMesh(sc)
         if not pt.initialize(a.width, a.height):
             raise SystemExit(pt.lastError())
         pt.renderFrames(a.spp, a.depth, copy=False)
@@ -59,7 +64,8 @@ def main():
         print(json.dumps({"scene": a.scene, **dict(combo), "msamples_s": round(st["segments"] / dt / 1e6, 1),
                           "trace_ms_step": round(st["traceMs"] / a.steps, 3),
                           "combine_ms_step": round(st["combineMs"] / a.steps, 3),
-                          "launches_step": st["traceLaunches"] // a.steps}), flush=True)
+                          "launches_step": st["traceLaunches"] // a.steps, "bvh_nodes": st["bvhNodes"],
+                          "bvh_depth": st["bvhDepth"]}), flush=True)
 
 
 if __name__ == "__main__":
