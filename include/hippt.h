@@ -189,7 +189,9 @@ enum {
     HIPPT_OPT_BVH_LEAF = 10,        /* max primitives per BVH leaf, 1..15; applies at the next upload */
     HIPPT_OPT_BVH_TRAVERSAL_COST = 11, /* SAH node-step cost in 1/100 primitive tests; next upload */
     HIPPT_OPT_BVH_MAX_DEPTH = 12,   /* interior-level bound (LDS stack per lane), 1..32; next upload */
-    HIPPT_OPT_DEVICE_ROWS = 13      /* hipptSetDevices split: 1 (default) interleaved rows, 0 bands; next Init */
+    HIPPT_OPT_DEVICE_ROWS = 13,     /* hipptSetDevices split: 1 (default) interleaved rows, 0 bands; next Init */
+    HIPPT_OPT_LEAF_EXIT = 14        /* node loop yields to the leaf loop once <= this many lanes lack a
+                                       leaf; -1 (default): automatic (2 for LDS scenes, else levels-6 in 0..16) */
 };
 bool hipptSetOption(int key, long long value);
 long long hipptGetOption(int key);

@@ -50,6 +50,7 @@ struct MeshParams {
     int full;              // 1: spheres or non-Lambertian materials present (general kernel)
     int waveThreshold;     // shade once fewer than this many lanes still traverse
     unsigned chunk;        // items per queue grab (multiple of 64)
+    unsigned leafExit;     // node loop exits once <= leafExit lanes still search for a leaf
 };
 
 // Running average + tonemap over a batch of per-sample radiances

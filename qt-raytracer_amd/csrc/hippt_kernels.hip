@@ -258,7 +258,7 @@ __global__ __launch_bounds__(kMeshBlock, HIPPT_MESH_WAVES_PER_EU) HIPPT_SGPR_ATT
         // ---- traversal: while-while over the BVH; leave once few lanes remain -------------
         do {
             prof<STATS>(pc, 2);
-            traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc);
+            traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit);
         } while (__popcll(__ballot(T.cur != kDone)) > unsigned(P.waveThreshold));
 
         // ---- shading: lanes whose traversal finished (ray_color step, RayTracer.h:579-596) ----

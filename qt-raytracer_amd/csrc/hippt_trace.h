@@ -401,7 +401,7 @@ __device__ __forceinline__ void begin(Trav &T) {
 template <int NODE_F4, bool STATS, bool FULL>
 __device__ __forceinline__ void traverse_round(Trav &T, const Ray &r, int *my, const float4 *nodes,
                                                const float4 *tris, unsigned long long &nvis,
-                                               unsigned long long &ntest, unsigned *pc) {
+                                               unsigned long long &ntest, unsigned *pc, unsigned leafExit = 0) {
     const float tmin = 0.001f;
     while (T.cur >= 0) {
         prof<STATS>(pc, 3);
@@ -435,7 +435,8 @@ __device__ __forceinline__ void traverse_round(Trav &T, const Ray &r, int *my, c
             T.leaf = T.cur;
             T.cur = T.sp > 0 ? my[T.sp -= kMeshBlock] : kDone;
         }
-        if (!__any(T.leaf == 0)) break;
+        // leave for the leaf loop once at most leafExit lanes still search for their first leaf
+        if (__popcll(__ballot(T.leaf == 0 && T.cur >= 0)) <= leafExit) break;
     }
     while (T.leaf != 0) {
         prof<STATS>(pc, 4);

@@ -25,7 +25,7 @@ def pt():
     t.useBuiltinScene(hippt.SCENE_SPHERE4)
     for k, v in ((hippt.OPT_WAVE_THRESHOLD, 32), (hippt.OPT_SCRATCH_MB, 4096), (hippt.OPT_CHUNK, 256),
                  (hippt.OPT_COUNT_TRAVERSAL, 0), (hippt.OPT_BLOCKS_PER_CU, 0), (hippt.OPT_LDS_SCENE, 1),
-                 (hippt.OPT_PATH_MODE, 0), (hippt.OPT_WAVEFRONT_SLOTS, 1 << 24)):
+                 (hippt.OPT_PATH_MODE, 0), (hippt.OPT_WAVEFRONT_SLOTS, 1 << 24), (hippt.OPT_LEAF_EXIT, -1)):
         t.setOption(k, v)
     t.resetStats()
     yield t
@@ -216,6 +216,25 @@ def test_mesh_wave_threshold_and_chunk_do_not_change_results(pt):
         assert pt.renderFrames(4, 8)
         got = pt.readback()
         if ref is None:
+            ref = got
+        else:
+            _assert_same(got[0], got[1], ref[0], ref[1])
+
+
+@pytest.mark.parametrize("name", ["blob70k", "cornell34"])
+def test_leaf_exit_does_not_change_results(pt, name):
+    """The node loop's early exit (HIPPT_OPT_LEAF_EXIT) only reorders work: identical images."""
+    sc = scenes.get_scene(name)
+    pt.uploadMesh(sc)
+    ref = None
+    for k in (0, 3, 16, 64, -1):
+        pt.setOption(hippt.OPT_LEAF_EXIT, k)
+        assert pt.initialize(56, 40)
+        assert pt.renderFrames(3, 8)
+        got = pt.readback()
+        if ref is None:
+            ora = po.MeshScene(sc, 56, 40).frames(0, 3, 8)
+            _assert_same(got[0], got[1], ora[0], ora[1])
             ref = got
         else:
             _assert_same(got[0], got[1], ref[0], ref[1])
