@@ -191,7 +191,9 @@ enum {
     HIPPT_OPT_BVH_MAX_DEPTH = 12,   /* interior-level bound (LDS stack per lane), 1..32; next upload */
     HIPPT_OPT_DEVICE_ROWS = 13,     /* hipptSetDevices split: 1 (default) interleaved rows, 0 bands; next Init */
     HIPPT_OPT_LEAF_EXIT = 14        /* node loop yields to the leaf loop once <= this many lanes lack a
-                                       leaf; -1 (default): automatic (2 for LDS scenes, else levels-6 in 0..16) */
+                                       leaf; -1 (default): automatic (4 for LDS scenes, else levels-6 in 0..16) */
+    , HIPPT_OPT_NODE_EXIT = 15      /* leaf loop yields to the node loop once <= this many lanes hold a leaf
+                                       (0 = never); -1 (default): 48 */
 };
 bool hipptSetOption(int key, long long value);
 long long hipptGetOption(int key);

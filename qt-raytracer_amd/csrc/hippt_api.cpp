@@ -111,6 +111,7 @@ struct State {
     long long scratchMB = 4096;
     unsigned chunk = 256;
     int leafExit = -1;  // -1: automatic from the tree depth and LDS residency
+    int nodeExit = -1;  // -1: automatic
     int blocksPerCu = 0;
     bool ldsScene = true;
     int pathMode = 0;             // 0 megakernel, 1 wavefront
@@ -553,10 +554,13 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.full = s.scene.full ? 1 : 0;
                         p.waveThreshold = s.waveThreshold;
                         p.chunk = s.chunk;
-                        // auto: deep, HBM/L2-resident trees profit from leaving the node loop early
-                        // (blob70k, 21 levels: 16 -> +27%); LDS scenes barely care (2 -> +0.3%)
+                        // Loop exits of the traversal round (measured): deep L2/HBM-resident
+                        // trees leave the node loop once <= levels-6 lanes still search (blob70k,
+                        // 21 levels: 9.8 -> 12.5 G), LDS scenes at 4; every scene leaves the leaf loop
+                        // once <= 48 lanes hold a leaf (Cornell 28.4 -> 31.3 G, blob -> 13.4 G).
                         p.leafExit = unsigned(s.leafExit >= 0 ? s.leafExit
-                                                              : ldsScene ? 2 : std::clamp(stackDepth - 6, 0, 16));
+                                                              : ldsScene ? 4 : std::clamp(stackDepth - 6, 0, 16));
+                        p.nodeExit = unsigned(s.nodeExit >= 0 ? s.nodeExit : 48);
                         if (s.pathMode == 1) {
                             if (!run_wavefront(c, p, cnt, err)) return false;
                         } else {
@@ -1064,6 +1068,10 @@ extern "C" bool hipptSetOption(int key, long long value) {
         if (value < -1 || value > 64) return false;
         s.leafExit = int(value);
         return true;
+    case HIPPT_OPT_NODE_EXIT:
+        if (value < -1 || value > 64) return false;
+        s.nodeExit = int(value);
+        return true;
     default: return false;
     }
 }
@@ -1085,6 +1093,7 @@ extern "C" long long hipptGetOption(int key) {
     case HIPPT_OPT_BVH_MAX_DEPTH: return s.bvh.maxDepth;
     case HIPPT_OPT_DEVICE_ROWS: return s.deviceInterleave ? 1 : 0;
     case HIPPT_OPT_LEAF_EXIT: return s.leafExit;
+    case HIPPT_OPT_NODE_EXIT: return s.nodeExit;
     default: return -1;
     }
 }

@@ -51,6 +51,7 @@ struct MeshParams {
     int waveThreshold;     // shade once fewer than this many lanes still traverse
     unsigned chunk;        // items per queue grab (multiple of 64)
     unsigned leafExit;     // node loop exits once <= leafExit lanes still search for a leaf
+    unsigned nodeExit;     // leaf loop exits once <= nodeExit lanes still hold a leaf (0: never)
 };
 
 // Running average + tonemap over a batch of per-sample radiances

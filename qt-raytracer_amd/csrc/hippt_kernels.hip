@@ -253,16 +253,16 @@ __global__ __launch_bounds__(kMeshBlock, HIPPT_MESH_WAVES_PER_EU) HIPPT_SGPR_ATT
                 }
             }
         }
-        if (!__any(T.cur != kDone)) break;
+        if (!__any(busy(T))) break;
 
         // ---- traversal: while-while over the BVH; leave once few lanes remain -------------
         do {
             prof<STATS>(pc, 2);
-            traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit);
-        } while (__popcll(__ballot(T.cur != kDone)) > unsigned(P.waveThreshold));
+            traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
+        } while (__popcll(__ballot(busy(T))) > unsigned(P.waveThreshold));
 
         // ---- shading: lanes whose traversal finished (ray_color step, RayTracer.h:579-596) ----
-        if (item != kNone && T.cur == kDone) {
+        if (item != kNone && !busy(T)) {
             prof<STATS>(pc, 6);
             ++segs;
             bool finished = false;

@@ -383,6 +383,9 @@ struct Trav {
     int bestI, bestO;
 };
 
+// Traversal still has work: nodes to visit or a postponed leaf to test.
+__device__ __forceinline__ bool busy(const Trav &T) { return T.cur != kDone || T.leaf != 0; }
+
 __device__ __forceinline__ void begin(Trav &T) {
     T.cur = 0;
     T.sp = 0;
@@ -401,7 +404,8 @@ __device__ __forceinline__ void begin(Trav &T) {
 template <int NODE_F4, bool STATS, bool FULL>
 __device__ __forceinline__ void traverse_round(Trav &T, const Ray &r, int *my, const float4 *nodes,
                                                const float4 *tris, unsigned long long &nvis,
-                                               unsigned long long &ntest, unsigned *pc, unsigned leafExit = 0) {
+                                               unsigned long long &ntest, unsigned *pc, unsigned leafExit = 0,
+                                               unsigned nodeExit = 0) {
     const float tmin = 0.001f;
     while (T.cur >= 0) {
         prof<STATS>(pc, 3);
@@ -488,6 +492,8 @@ __device__ __forceinline__ void traverse_round(Trav &T, const Ray &r, int *my, c
             T.leaf = T.cur;
             T.cur = T.sp > 0 ? my[T.sp -= kMeshBlock] : kDone;
         }
+        // back to the node loop once at most nodeExit lanes still hold a leaf (they keep it)
+        if (nodeExit && __popcll(__ballot(T.leaf != 0)) <= nodeExit) break;
     }
 }
 

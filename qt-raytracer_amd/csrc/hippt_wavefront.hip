@@ -162,11 +162,11 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
             }
         }
         need = false;
-        if (!__any(T.cur != kDone)) break;
+        if (!__any(busy(T))) break;
         do {
-            traverse_round<LDS_SCENE ? 5 : 4, false, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit);
-        } while (__popcll(__ballot(T.cur != kDone)) > unsigned(P.waveThreshold));
-        if (slot != kNone && T.cur == kDone) {
+            traverse_round<LDS_SCENE ? 5 : 4, false, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
+        } while (__popcll(__ballot(busy(T))) > unsigned(P.waveThreshold));
+        if (slot != kNone && !busy(T)) {
             *reinterpret_cast<float2 *>(W.st + 4 * size_t(slot) + 3) = make_float2(T.bestT, __int_as_float(T.bestI));
             slot = kNone;
             need = true;

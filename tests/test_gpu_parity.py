@@ -25,7 +25,8 @@ def pt():
     t.useBuiltinScene(hippt.SCENE_SPHERE4)
     for k, v in ((hippt.OPT_WAVE_THRESHOLD, 32), (hippt.OPT_SCRATCH_MB, 4096), (hippt.OPT_CHUNK, 256),
                  (hippt.OPT_COUNT_TRAVERSAL, 0), (hippt.OPT_BLOCKS_PER_CU, 0), (hippt.OPT_LDS_SCENE, 1),
-                 (hippt.OPT_PATH_MODE, 0), (hippt.OPT_WAVEFRONT_SLOTS, 1 << 24), (hippt.OPT_LEAF_EXIT, -1)):
+                 (hippt.OPT_PATH_MODE, 0), (hippt.OPT_WAVEFRONT_SLOTS, 1 << 24), (hippt.OPT_LEAF_EXIT, -1),
+                 (hippt.OPT_NODE_EXIT, -1)):
         t.setOption(k, v)
     t.resetStats()
     yield t
@@ -221,14 +222,17 @@ def test_mesh_wave_threshold_and_chunk_do_not_change_results(pt):
             _assert_same(got[0], got[1], ref[0], ref[1])
 
 
-@pytest.mark.parametrize("name", ["blob70k", "cornell34"])
-def test_leaf_exit_does_not_change_results(pt, name):
-    """The node loop's early exit (HIPPT_OPT_LEAF_EXIT) only reorders work: identical images."""
+@pytest.mark.parametrize("name,mode", [("blob70k", 0), ("cornell34", 0), ("blob70k", 1)])
+def test_loop_exits_do_not_change_results(pt, name, mode):
+    """The node and leaf loops' early exits (HIPPT_OPT_LEAF_EXIT / NODE_EXIT) only reorder work:
+    identical images, megakernel and wavefront."""
     sc = scenes.get_scene(name)
     pt.uploadMesh(sc)
+    pt.setOption(hippt.OPT_PATH_MODE, mode)
     ref = None
-    for k in (0, 3, 16, 64, -1):
+    for k, n in ((0, 0), (3, 0), (16, 0), (64, 0), (-1, 0), (0, 8), (-1, 16), (16, 64), (-1, -1)):
         pt.setOption(hippt.OPT_LEAF_EXIT, k)
+        pt.setOption(hippt.OPT_NODE_EXIT, n)
         assert pt.initialize(56, 40)
         assert pt.renderFrames(3, 8)
         got = pt.readback()

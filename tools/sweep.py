@@ -24,7 +24,8 @@ from hippt import scenes  # noqa: E402
 KEYS = {"wave": hippt.OPT_WAVE_THRESHOLD, "chunk": hippt.OPT_CHUNK, "scratch": hippt.OPT_SCRATCH_MB,
         "bpc": hippt.OPT_BLOCKS_PER_CU, "lds": hippt.OPT_LDS_SCENE, "mode": hippt.OPT_PATH_MODE,
         "slots": hippt.OPT_WAVEFRONT_SLOTS, "leaf": hippt.OPT_BVH_LEAF, "tcost": hippt.OPT_BVH_TRAVERSAL_COST,
-        "depth": hippt.OPT_BVH_MAX_DEPTH, "leafexit": hippt.OPT_LEAF_EXIT}
+        "depth": hippt.OPT_BVH_MAX_DEPTH, "leafexit": hippt.OPT_LEAF_EXIT,
+        "nodeexit": hippt.OPT_NODE_EXIT}
 REUPLOAD = {"leaf", "tcost", "depth"}  # build parameters: take effect at the next upload
 
 
