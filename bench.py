@@ -26,6 +26,7 @@ Also reported on rank 0:
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import subprocess
@@ -130,15 +131,21 @@ def cpu_baseline(args, scene) -> dict | None:
 
 
 def load_pmc(args, workload: str):
-    path = args.pmc or os.path.join(REPO, "profiles", "pmc_summary.json")
-    try:
-        with open(path) as f:
-            d = json.load(f)
-    except (OSError, ValueError):
-        return None
-    if d.get("workload") != workload:
-        return None
-    return d.get("hbm_bytes_per_launch")
+    """HBM bytes per launch from a tools/profile.sh summary of this exact workload: --pmc, else
+    profiles/pmc_summary.json (the default workload), else the newest profiles/<tag>_pmc.json."""
+    prof = os.path.join(REPO, "profiles")
+    paths = [args.pmc] if args.pmc else (
+        [os.path.join(prof, "pmc_summary.json")]
+        + sorted(glob.glob(os.path.join(prof, "*_pmc.json")), reverse=True))
+    for path in paths:
+        try:
+            with open(path) as f:
+                d = json.load(f)
+        except (OSError, ValueError):
+            continue
+        if d.get("workload") == workload:
+            return d.get("hbm_bytes_per_launch")
+    return None
 
 
 def main():

@@ -366,7 +366,9 @@ size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris) {
 
 size_t mesh_lds_scene_limit() { return 24u << 10; }
 
-static constexpr int kMaxResidentBlocks = 7;
+// waves a SIMD holds under the SGPR budget: 800 SGPRs per SIMD, 16 of them reserved per wave
+// for the trap handler (one block = 4 waves = one wave per SIMD)
+static constexpr int kMaxResidentBlocks = 800 / (HIPPT_NUM_SGPR + 16) < 8 ? 800 / (HIPPT_NUM_SGPR + 16) : 8;
 
 using MeshFn = void (*)(MeshParams);
 static MeshFn mesh_fn(bool count, bool lds, bool full) {
@@ -401,9 +403,8 @@ int mesh_blocks_per_cu(bool countTraversal, bool full, int stackDepth, int ldsNo
     hipError_t e =
         hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mesh_fn(countTraversal, lds, full), kMeshBlock, bytes);
     if (e != hipSuccess || n <= 0) n = 1;
-    // the query ignores the trap handler's SGPRs: with HIPPT_NUM_SGPR (<= 96) a SIMD holds at
-    // most 7 waves, i.e. 7 blocks of 4 waves per CU; a larger persistent grid leaves blocks
-    // waiting for a slot until others finish
+    // the query ignores the trap handler's SGPRs (kMaxResidentBlocks): a larger persistent grid
+    // leaves blocks waiting for a slot until others finish
     return std::min(n, kMaxResidentBlocks);
 }
 

@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
     T.bestI = -1;
     T.bestO = 0x7fffffff;
     unsigned long long nvis = 0, ntest = 0;
-    unsigned pc[16];  // phase profile slots (unused here)
+    unsigned pc[16] = {};  // phase profile slots (not reported by the wavefront path)
     for (;;) {
         while (left && __ballot(need)) {
             const unsigned qi =
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
         need = false;
         if (!__any(busy(T))) break;
         do {
-            traverse_round<LDS_SCENE ? 5 : 4, false, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
+            traverse_round<LDS_SCENE ? 5 : 4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
         } while (__popcll(__ballot(busy(T))) > unsigned(P.waveThreshold));
         if (slot != kNone && !busy(T)) {
             *reinterpret_cast<float2 *>(W.st + 4 * size_t(slot) + 3) = make_float2(T.bestT, __int_as_float(T.bestI));

@@ -364,9 +364,11 @@ def test_full_size_1080p_rows_and_determinism(pt):
         _assert_same(a[0][y0:y0 + 2], a[1][y0:y0 + 2], ora[0], ora[1])
 
 
-def test_counting_mode_reports_traversal(pt):
+@pytest.mark.parametrize("mode", [0, 1], ids=["megakernel", "wavefront"])
+def test_counting_mode_reports_traversal(pt, mode):
     sc = scenes.blob70k()
     pt.uploadMesh(sc)
+    pt.setOption(hippt.OPT_PATH_MODE, mode)
     pt.setOption(hippt.OPT_COUNT_TRAVERSAL, 1)
     assert pt.initialize(64, 32)
     assert pt.renderFrames(2, 8)

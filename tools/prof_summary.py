@@ -95,7 +95,10 @@ def main():
     }
     prof_dir = os.path.join(repo, "profiles")
     os.makedirs(prof_dir, exist_ok=True)
-    with open(os.path.join(prof_dir, "pmc_summary.json"), "w") as f:
+    # bench.py reads pmc_summary.json for roofline.traffic of its default workload (Cornell);
+    # any other workload keeps its counters beside its summary
+    default = workload.startswith("cornell34 1920x1080 64spp depth8") and "wavefront" not in workload
+    with open(os.path.join(prof_dir, "pmc_summary.json" if default else f"{tag}_pmc.json"), "w") as f:
         json.dump(summary, f, indent=1)
     stats_csv = open(os.path.join(root, "kt", "run_kernel_stats.csv")).read()
     with open(os.path.join(prof_dir, f"{tag}_summary.md"), "w") as f:
