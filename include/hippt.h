@@ -194,6 +194,8 @@ enum {
                                        leaf; -1 (default): automatic (4 for LDS scenes, else levels-6 in 0..16) */
     , HIPPT_OPT_NODE_EXIT = 15      /* leaf loop yields to the node loop once <= this many lanes hold a leaf
                                        (0 = never); -1 (default): 48 */
+    , HIPPT_OPT_BVH_SAH = 16        /* BVH split search: 1 (default) all axes, exact sweep SAH (32 bins on
+                                       nodes over 65536 primitives); 0: 16 bins on the longest axis; next upload */
 };
 bool hipptSetOption(int key, long long value);
 long long hipptGetOption(int key);

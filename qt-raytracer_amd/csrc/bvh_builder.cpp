@@ -31,7 +31,16 @@ struct Prim {
     int id;
 };
 
-constexpr int kBins = 16;
+constexpr int kMaxBins = 32;
+constexpr int kSweepMax = 1 << 16;  // exact sweep SAH up to this many primitives per node
+
+// Centroid order on one axis, ties by primitive id (a total order: deterministic splits).
+struct by_centroid {
+    int axis;
+    bool operator()(const Prim &p, const Prim &q) const {
+        return p.c[axis] < q.c[axis] || (p.c[axis] == q.c[axis] && p.id < q.id);
+    }
+};
 
 int ceil_log2(long long v) {
     int r = 0;
@@ -66,21 +75,43 @@ public:
             mid = n <= par_.maxLeaf ? -1 : median_split(b, e, axis);
         } else if (ext[axis] <= 0.0f) {
             mid = n > par_.maxLeaf ? b + n / 2 : -1;  // coincident centroids: split by index
-        } else {
+        } else if (par_.sahMode == 0) {
             float best_cost;
             int best_bin;
-            sah(b, e, axis, cb, best_cost, best_bin);
-            const float leaf_cost = float(n);
-            if (n <= par_.maxLeaf && leaf_cost <= best_cost) {
+            sah(b, e, axis, cb, best_cost, best_bin, 16);
+            if (n <= par_.maxLeaf && float(n) <= best_cost) {
                 mid = -1;
             } else {
-                const float lo = cb.lo[axis], scale = kBins / ext[axis];
-                auto it = std::partition(prims_.begin() + b, prims_.begin() + e, [&](const Prim &p) {
-                    int bin = std::min(kBins - 1, int((p.c[axis] - lo) * scale));
-                    return bin <= best_bin;
-                });
-                mid = int(it - prims_.begin());
+                mid = partition_bins(b, e, axis, cb, best_bin, 16);
                 if (mid == b || mid == e) mid = median_split(b, e, axis);
+            }
+        } else {
+            // best split over all three axes: exact sweep SAH up to kSweepMax primitives, 32 bins above
+            float best_cost = INFINITY;
+            int best_axis = -1, best_pos = -1;
+            for (int a = 0; a < 3; ++a) {
+                if (!(ext[a] > 0.0f)) continue;
+                float cost;
+                int pos;
+                if (n <= kSweepMax) {
+                    sweep(b, e, a, cost, pos);
+                } else {
+                    sah(b, e, a, cb, cost, pos, 32);
+                }
+                if (cost < best_cost) {
+                    best_cost = cost;
+                    best_axis = a;
+                    best_pos = pos;
+                }
+            }
+            if (best_axis < 0 || (n <= par_.maxLeaf && float(n) <= best_cost)) {
+                mid = n <= par_.maxLeaf ? -1 : median_split(b, e, axis);
+            } else if (n <= kSweepMax) {
+                mid = b + best_pos;  // left count
+                std::nth_element(prims_.begin() + b, prims_.begin() + mid, prims_.begin() + e, by_centroid{best_axis});
+            } else {
+                mid = partition_bins(b, e, best_axis, cb, best_pos, 32);
+                if (mid == b || mid == e) mid = median_split(b, e, best_axis);
             }
         }
         if (mid < 0) {
@@ -119,40 +150,71 @@ public:
 private:
     int median_split(int b, int e, int axis) {
         const int mid = b + (e - b) / 2;
-        std::nth_element(prims_.begin() + b, prims_.begin() + mid, prims_.begin() + e,
-                         [axis](const Prim &p, const Prim &q) {
-                             return p.c[axis] < q.c[axis] || (p.c[axis] == q.c[axis] && p.id < q.id);
-                         });
+        std::nth_element(prims_.begin() + b, prims_.begin() + mid, prims_.begin() + e, by_centroid{axis});
         return mid;
     }
 
-    void sah(int b, int e, int axis, const Box &cb, float &best_cost, int &best_bin) {
-        Box bins[kBins];
-        int counts[kBins] = {0};
-        const float lo = cb.lo[axis], scale = kBins / (cb.hi[axis] - cb.lo[axis]);
+    int partition_bins(int b, int e, int axis, const Box &cb, int best_bin, int nb) {
+        const float lo = cb.lo[axis], scale = float(nb) / (cb.hi[axis] - cb.lo[axis]);
+        auto it = std::partition(prims_.begin() + b, prims_.begin() + e, [&](const Prim &p) {
+            return std::min(nb - 1, int((p.c[axis] - lo) * scale)) <= best_bin;
+        });
+        return int(it - prims_.begin());
+    }
+
+    // Exact SAH over the centroid order on `axis`: best_pos = primitives left of the split.
+    void sweep(int b, int e, int axis, float &best_cost, int &best_pos) {
+        const int n = e - b;
+        order_.assign(prims_.begin() + b, prims_.begin() + e);
+        std::sort(order_.begin(), order_.end(), by_centroid{axis});
+        right_.resize(size_t(n));
+        Box acc;
+        for (int i = n - 1; i > 0; --i) {
+            acc.grow(order_[size_t(i)].lo, order_[size_t(i)].hi);
+            right_[size_t(i)] = acc.area();
+        }
+        acc.grow(order_[0].lo, order_[0].hi);
+        const float pa = std::max(acc.area(), 1e-30f);
+        best_cost = INFINITY;
+        best_pos = n / 2;
+        Box left;
+        for (int i = 1; i < n; ++i) {
+            left.grow(order_[size_t(i - 1)].lo, order_[size_t(i - 1)].hi);
+            const float cost = par_.traversalCost + (left.area() * float(i) + right_[size_t(i)] * float(n - i)) / pa;
+            if (cost < best_cost) {
+                best_cost = cost;
+                best_pos = i;
+            }
+        }
+    }
+
+    void sah(int b, int e, int axis, const Box &cb, float &best_cost, int &best_bin, int nb) {
+        Box bins[kMaxBins];
+        int counts[kMaxBins] = {0};
+        const float lo = cb.lo[axis], scale = float(nb) / (cb.hi[axis] - cb.lo[axis]);
         for (int i = b; i < e; ++i) {
-            int bin = std::min(kBins - 1, int((prims_[i].c[axis] - lo) * scale));
+            int bin = std::min(nb - 1, int((prims_[i].c[axis] - lo) * scale));
             ++counts[bin];
             bins[bin].grow(prims_[i].lo, prims_[i].hi);
         }
-        float right_area[kBins];
-        int right_count[kBins];
+        float right_area[kMaxBins];
+        int right_count[kMaxBins];
         Box acc;
         int cnt = 0;
-        for (int i = kBins - 1; i > 0; --i) {
+        for (int i = nb - 1; i > 0; --i) {
             acc.grow(bins[i]);
             cnt += counts[i];
             right_area[i] = acc.area();
             right_count[i] = cnt;
         }
         Box parent;
-        for (int i = 0; i < kBins; ++i) parent.grow(bins[i]);
+        for (int i = 0; i < nb; ++i) parent.grow(bins[i]);
         const float pa = std::max(parent.area(), 1e-30f);
         best_cost = INFINITY;
-        best_bin = kBins / 2 - 1;
+        best_bin = nb / 2 - 1;
         Box left;
         int lcnt = 0;
-        for (int i = 0; i < kBins - 1; ++i) {
+        for (int i = 0; i < nb - 1; ++i) {
             left.grow(bins[i]);
             lcnt += counts[i];
             if (lcnt == 0 || right_count[i + 1] == 0) continue;
@@ -165,6 +227,8 @@ private:
         }
     }
 
+    std::vector<Prim> order_;
+    std::vector<float> right_;
     std::vector<Prim> &prims_;
     float pad_;
     BvhParams par_;
@@ -228,7 +292,8 @@ bool build_bvh_boxes(const float *boxes, int numPrims, float extentHint, Bvh &ou
     return true;
 }
 
-bool build_bvh(const float *verts, int numTris, float extentHint, Bvh &out, std::string &err) {
+bool build_bvh(const float *verts, int numTris, float extentHint, Bvh &out, std::string &err,
+               const BvhParams &params) {
     if (numTris <= 0) {
         err = "BVH requires at least one triangle";
         return false;
@@ -242,7 +307,7 @@ bool build_bvh(const float *verts, int numTris, float extentHint, Bvh &out, std:
             bx[3 + a] = std::max(v[a], std::max(v[3 + a], v[6 + a]));
         }
     }
-    return build_bvh_boxes(boxes.data(), numTris, extentHint, out, err);
+    return build_bvh_boxes(boxes.data(), numTris, extentHint, out, err, params);
 }
 
 }  // namespace hippt

@@ -26,6 +26,7 @@ struct BvhParams {
     int maxLeaf = kMaxLeafTris;
     float traversalCost = 1.0f;
     int maxDepth = kStackDepth;
+    int sahMode = 1;  // 0: 16 bins on the longest centroid axis; 1: all axes, exact sweep (32 bins on big nodes)
 };
 
 struct Bvh {
@@ -38,7 +39,8 @@ struct Bvh {
 // verts: numTris * 9 floats.  extentHint: largest |coordinate| any ray origin can have
 // (camera position); boxes are padded by max(|coord|, extentHint) * 2^-16 so the
 // kernel's FMA slab test is conservative.
-bool build_bvh(const float *verts, int numTris, float extentHint, Bvh &out, std::string &err);
+bool build_bvh(const float *verts, int numTris, float extentHint, Bvh &out, std::string &err,
+               const BvhParams &params = BvhParams());
 // General primitives: boxes = numPrims * 6 floats (lo xyz, hi xyz); `order` maps leaf order
 // to the primitive index.
 bool build_bvh_boxes(const float *boxes, int numPrims, float extentHint, Bvh &out, std::string &err,

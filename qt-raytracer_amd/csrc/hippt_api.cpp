@@ -1072,6 +1072,10 @@ extern "C" bool hipptSetOption(int key, long long value) {
         if (value < -1 || value > 64) return false;
         s.nodeExit = int(value);
         return true;
+    case HIPPT_OPT_BVH_SAH:
+        if (value != 0 && value != 1) return false;
+        s.bvh.sahMode = int(value);
+        return true;
     default: return false;
     }
 }
@@ -1094,6 +1098,7 @@ extern "C" long long hipptGetOption(int key) {
     case HIPPT_OPT_DEVICE_ROWS: return s.deviceInterleave ? 1 : 0;
     case HIPPT_OPT_LEAF_EXIT: return s.leafExit;
     case HIPPT_OPT_NODE_EXIT: return s.nodeExit;
+    case HIPPT_OPT_BVH_SAH: return s.bvh.sahMode;
     default: return -1;
     }
 }
@@ -1104,7 +1109,12 @@ extern "C" const char *hipptLastError(void) { return S().error; }
 extern "C" hipptBvh *hipptBvhBuild(const float *verts, int numTris, float extentHint, const char **err) {
     auto *b = new hipptBvh();
     std::string msg;
-    if (!verts || !hippt::build_bvh(verts, numTris, extentHint, b->bvh, msg)) {
+    hippt::BvhParams params;
+    {
+        std::lock_guard<std::mutex> g(S().mu);
+        params = S().bvh;  // the build options an upload would use
+    }
+    if (!verts || !hippt::build_bvh(verts, numTris, extentHint, b->bvh, msg, params)) {
         delete b;
         std::lock_guard<std::mutex> g(S().mu);
         fail(err, msg.empty() ? "null vertex pointer" : msg);

@@ -40,6 +40,7 @@ OPT_BVH_MAX_DEPTH = 12
 OPT_DEVICE_ROWS = 13
 OPT_LEAF_EXIT = 14
 OPT_NODE_EXIT = 15
+OPT_BVH_SAH = 16
 
 # Every symbol include/hippt.h declares (checked by tests/test_abi_cpu.py).
 EXPORTS = (

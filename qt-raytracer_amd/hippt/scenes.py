@@ -163,12 +163,17 @@ def blob_mesh(nu: int = 256, nv: int = 136, center=(278.0, 180.0, 278.0), radius
 
 
 def blob70k() -> Scene:
+    return blob_scene(256, 136, "blob70k")
+
+
+def blob_scene(nu: int, nv: int, name: str | None = None) -> Scene:
+    """blob70k's walls around a blob of nu x nv quads (blob70k: 256 x 136)."""
     tris, mats = _walls()
     walls = np.asarray(tris, dtype=np.float64).astype(np.float32)
-    blob = blob_mesh()
+    blob = blob_mesh(nu, nv)
     verts = np.concatenate([walls, blob], axis=0)
     tri_mat = np.concatenate([np.asarray(mats, np.int32), np.zeros(len(blob), np.int32)])
-    return Scene(name="blob70k", verts=np.ascontiguousarray(verts), tri_mat=tri_mat,
+    return Scene(name=name or f"blob{nu}x{nv}", verts=np.ascontiguousarray(verts), tri_mat=tri_mat,
                  albedo=np.asarray([WHITE, GREEN, RED], dtype=np.float32))
 
 

@@ -31,8 +31,16 @@ def _walk(nodes):
     return leaves, depth
 
 
+@pytest.fixture(params=[1, 0], ids=["sweep-sah", "binned-sah"])
+def sah_mode(request):
+    lib = hippt.load_library()
+    assert lib.hipptSetOption(hippt.OPT_BVH_SAH, request.param)
+    yield request.param
+    lib.hipptSetOption(hippt.OPT_BVH_SAH, 1)
+
+
 @pytest.mark.parametrize("name", ["cornell34", "blob70k"])
-def test_bvh_covers_every_triangle_once_and_bounds_children(name):
+def test_bvh_covers_every_triangle_once_and_bounds_children(name, sah_mode):
     sc = scenes.get_scene(name)
     bvh = hippt.Bvh(sc.verts, extent_hint=800.0)
     assert sorted(bvh.order.tolist()) == list(range(sc.num_tris))

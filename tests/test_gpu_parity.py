@@ -26,7 +26,7 @@ def pt():
     for k, v in ((hippt.OPT_WAVE_THRESHOLD, 32), (hippt.OPT_SCRATCH_MB, 4096), (hippt.OPT_CHUNK, 256),
                  (hippt.OPT_COUNT_TRAVERSAL, 0), (hippt.OPT_BLOCKS_PER_CU, 0), (hippt.OPT_LDS_SCENE, 1),
                  (hippt.OPT_PATH_MODE, 0), (hippt.OPT_WAVEFRONT_SLOTS, 1 << 24), (hippt.OPT_LEAF_EXIT, -1),
-                 (hippt.OPT_NODE_EXIT, -1)):
+                 (hippt.OPT_NODE_EXIT, -1), (hippt.OPT_BVH_SAH, 1)):
         t.setOption(k, v)
     t.resetStats()
     yield t

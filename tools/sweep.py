@@ -25,8 +25,8 @@ KEYS = {"wave": hippt.OPT_WAVE_THRESHOLD, "chunk": hippt.OPT_CHUNK, "scratch": h
         "bpc": hippt.OPT_BLOCKS_PER_CU, "lds": hippt.OPT_LDS_SCENE, "mode": hippt.OPT_PATH_MODE,
         "slots": hippt.OPT_WAVEFRONT_SLOTS, "leaf": hippt.OPT_BVH_LEAF, "tcost": hippt.OPT_BVH_TRAVERSAL_COST,
         "depth": hippt.OPT_BVH_MAX_DEPTH, "leafexit": hippt.OPT_LEAF_EXIT,
-        "nodeexit": hippt.OPT_NODE_EXIT}
-REUPLOAD = {"leaf", "tcost", "depth"}  # build parameters: take effect at the next upload
+        "nodeexit": hippt.OPT_NODE_EXIT, "sah": hippt.OPT_BVH_SAH}
+REUPLOAD = {"leaf", "tcost", "depth", "sah"}  # build parameters: take effect at the next upload
 
 
 def main():
@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--spp", type=int, default=64)
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--blob", default=None, help="NU,NV: blob70k's walls + a blob of NU x NV quads")
+    ap.add_argument("--count", action="store_true", help="report node visits / primitive tests per segment")
     ap.add_argument("grid", nargs="*")
     a = ap.parse_args()
     axes = []
@@ -46,6 +48,10 @@ def main():
     pt = hippt.PathTracer()
     pt.setDevices([0])
     sc = scenes.get_scene(a.scene)
+    if a.blob:
+        nu, nv = map(int, a.blob.split(","))
+        sc = scenes.blob_scene(nu, nv)
+        a.scene = f"blob{nu}x{nv}"
     pt.uploadMesh(sc)
     for combo in itertools.product(*axes) if axes else [()]:
         for k, v in combo:
@@ -55,6 +61,15 @@ def main():
         if not pt.initialize(a.width, a.height):
             raise SystemExit(pt.lastError())
         pt.renderFrames(a.spp, a.depth, copy=False)
+        extra = {}
+        if a.count:
+            pt.resetStats()
+            pt.setOption(hippt.OPT_COUNT_TRAVERSAL, 1)
+            pt.renderFrames(a.spp, a.depth, copy=False)
+            pt.setOption(hippt.OPT_COUNT_TRAVERSAL, 0)
+            c = pt.stats()
+            extra = {"visits_per_seg": round(c["nodeVisits"] / c["segments"], 3),
+                     "tests_per_seg": round(c["triTests"] / c["segments"], 3), "triangles": int(sc.num_tris)}
         pt.resetStats()
         t0 = time.perf_counter()
         for _ in range(a.steps):
@@ -66,7 +81,7 @@ def main():
                           "trace_ms_step": round(st["traceMs"] / a.steps, 3),
                           "combine_ms_step": round(st["combineMs"] / a.steps, 3),
                           "launches_step": st["traceLaunches"] // a.steps, "bvh_nodes": st["bvhNodes"],
-                          "bvh_depth": st["bvhDepth"]}), flush=True)
+                          "bvh_depth": st["bvhDepth"], **extra}), flush=True)
 
 
 if __name__ == "__main__":
