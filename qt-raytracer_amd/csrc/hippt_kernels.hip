@@ -153,7 +153,9 @@ __global__ __launch_bounds__(256) void sphere4_kernel(Sphere4Params P) {
 // Mesh megakernel.
 // =========================================================================================
 
-// Build knob (experiments): minimum waves per SIMD the register allocator must allow.
+// Build knob (experiments): minimum waves per SIMD the register allocator must allow.  The
+// general (FULL) kernel is held to 7 (<= 72 VGPRs, as many waves as the SGPR budget allows)
+// instead of the 6 its 73 VGPRs would give.
 #ifndef HIPPT_MESH_WAVES_PER_EU
 #define HIPPT_MESH_WAVES_PER_EU 1
 #endif
@@ -181,7 +183,7 @@ __device__ unsigned long long g_timeline[65536 * 6];
 #define HIPPT_SGPR_ATTR __attribute__((amdgpu_num_sgpr(HIPPT_NUM_SGPR)))
 
 template <bool STATS, bool LDS_SCENE, bool FULL>
-__global__ __launch_bounds__(kMeshBlock, HIPPT_MESH_WAVES_PER_EU) HIPPT_SGPR_ATTR void mesh_kernel(MeshParams P) {
+__global__ __launch_bounds__(kMeshBlock, FULL ? 7 : HIPPT_MESH_WAVES_PER_EU) HIPPT_SGPR_ATTR void mesh_kernel(MeshParams P) {
 #ifdef HIPPT_DEBUG_TIMELINE
     const unsigned tlw = blockIdx.x * 4u + (threadIdx.x >> 6);
     unsigned long long tlDrained = 0, tlItems = 0;
