@@ -15,7 +15,8 @@ closest-hit query), so nothing is estimated.
 Also reported on rank 0:
   roofline      the mesh kernel's algorithmic bytes per launch / its mean launch time (HIP
                 events on the library's stream, timed region), against the 8 TB/s HBM peak;
-                bytes per launch from a counted (untimed) pass: 64 B per BVH node visit,
+                bytes per launch from a counted (untimed) pass: 64 B per 2-wide BVH node
+                visit (112 B per 4-wide visit),
                 48 B per triangle test, 32 B per shaded hit, 12 B per sample written
                 (DESIGN.md §Roofline).  traffic = PMC-measured HBM bytes per launch from
                 profiles/ when a matching summary exists, else null.
@@ -42,6 +43,7 @@ sys.path.insert(0, os.path.join(REPO, "qt-raytracer_amd"))
 METRIC = "Msamples/s (rays×bounces/s) at 1920×1080, 8 bounces; 1/2/4/8-GPU scaling"
 HBM_PEAK_GBS = 8000.0
 BYTES_NODE, BYTES_TRI, BYTES_SHADE, BYTES_SAMPLE = 64, 48, 32, 12
+BYTES_NODE4 = 112  # 4-wide node: 4 child boxes + 4 child codes
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector (= FP32 MFMA) peak
 FLOP_NODE, FLOP_TRI, FLOP_SHADE = 40, 55, 100  # SURVEY.md §8(d) secondary figure
 
@@ -213,6 +215,7 @@ def main():
     step()
     device_sync(pt)
     counted = pt.stats()
+    bvh_width = pt._lib.hipptActiveBvhWidth()  # the tree nodeVisits count (2- or 4-wide)
     pt.setOption(hippt.OPT_COUNT_TRAVERSAL, 0)
 
     for _ in range(args.warmup):
@@ -242,11 +245,13 @@ def main():
 
     # roofline of the dominant (mesh) kernel, from this rank's counted pass and live events
     launches = max(1, st["traceLaunches"] // max(1, args.steps))
-    alg_bytes_step = (BYTES_NODE * counted["nodeVisits"] + BYTES_TRI * counted["triTests"]
+    bytes_node = BYTES_NODE if bvh_width != 4 else BYTES_NODE4
+    flop_node = FLOP_NODE if bvh_width != 4 else 2 * FLOP_NODE
+    alg_bytes_step = (bytes_node * counted["nodeVisits"] + BYTES_TRI * counted["triTests"]
                       + BYTES_SHADE * (counted["segments"] - counted["pixelSamples"])
                       + BYTES_SAMPLE * counted["pixelSamples"])
     alg_bytes_launch = alg_bytes_step / launches
-    flops_launch = (FLOP_NODE * counted["nodeVisits"] + FLOP_TRI * counted["triTests"]
+    flops_launch = (flop_node * counted["nodeVisits"] + FLOP_TRI * counted["triTests"]
                     + FLOP_SHADE * counted["segments"]) / launches
     mean_launch_ms = st["traceMs"] / max(1, st["traceLaunches"])
     achieved = alg_bytes_launch / (mean_launch_ms * 1e-3) / 1e9 if mean_launch_ms > 0 else 0.0
@@ -283,7 +288,7 @@ def main():
                 "mpixel_samples_per_s": round(samples / elapsed_max / 1e6, 3),
                 "trace_ms_per_step": round(st["traceMs"] / args.steps, 4),
                 "combine_ms_per_step": round(st["combineMs"] / args.steps, 4),
-                "bvh_nodes": st["bvhNodes"], "bvh_depth": st["bvhDepth"],
+                "bvh_nodes": st["bvhNodes"], "bvh_depth": st["bvhDepth"], "bvh_width": bvh_width,
                 "wave_threshold": pt._lib.hipptGetOption(hippt.OPT_WAVE_THRESHOLD),
                 "chunk": pt._lib.hipptGetOption(hippt.OPT_CHUNK),
                 "image_crc32": zlib.crc32(full.tobytes()) & 0xFFFFFFFF,
@@ -300,7 +305,7 @@ def main():
                          "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(flops_launch / (mean_launch_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4)
                          if mean_launch_ms else 0.0,
-                         "model": "40 FLOP/node visit (2 slab tests), 55/triangle test, 100/shading step"},
+                         "model": "20 FLOP/slab test (2 per 2-wide, 4 per 4-wide node visit), 55/triangle test, 100/shading step"},
             },
             "cpu_baseline": cpu,
         }

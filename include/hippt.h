@@ -196,9 +196,16 @@ enum {
                                        (0 = never); -1 (default): 48 */
     , HIPPT_OPT_BVH_SAH = 16        /* BVH split search: 1 (default) all axes, exact sweep SAH (32 bins on
                                        nodes over 65536 primitives); 0: 16 bins on the longest axis; next upload */
+    , HIPPT_OPT_BVH_WIDTH = 17      /* megakernel traversal over the 4-wide (4) or 2-wide (2) BVH; 0 (default):
+                                       4-wide when the scene fits in LDS as 4-wide nodes, else 2-wide */
+    , HIPPT_OPT_STACK_CAP = 18      /* 4-wide traversal: LDS stack entries per lane, 4..30 (deeper stacks spill
+                                       to global memory); 0 (default): the tree's bound, at most 19 (30 for
+                                       LDS scenes) */
 };
 bool hipptSetOption(int key, long long value);
 long long hipptGetOption(int key);
+/* BVH width (2 or 4) the last mesh render traversed (0 before any): what nodeVisits count. */
+int hipptActiveBvhWidth(void);
 
 const char *hipptLastError(void);
 
@@ -212,6 +219,15 @@ int hipptBvhDepth(const hipptBvh *bvh);
 /* nodes: NodeCount*16 words; triOrder: numTris ints (leaf order -> original triangle index). */
 void hipptBvhCopy(const hipptBvh *bvh, uint32_t *nodes, int *triOrder);
 void hipptBvhFree(hipptBvh *bvh);
+/* The 4-wide tree the megakernel traverses (HIPPT_OPT_BVH_WIDTH 4), collapsed from the 2-wide
+ * one (same leaves and triangle order).  Node = 32 words: lo.x[4] hi.x[4] lo.y[4] hi.y[4]
+ * lo.z[4] hi.z[4] (floats), child[4] (codes as above; an unused slot holds an empty leaf under
+ * a box far outside the scene), 4 reserved.  Depth = nodes on the deepest path; StackBound =
+ * the most traversal-stack entries any ray can need. */
+int hipptBvh4NodeCount(const hipptBvh *bvh);
+int hipptBvh4Depth(const hipptBvh *bvh);
+int hipptBvh4StackBound(const hipptBvh *bvh);
+void hipptBvh4Copy(const hipptBvh *bvh, uint32_t *nodes);
 
 #ifdef __cplusplus
 }

@@ -310,4 +310,83 @@ bool build_bvh(const float *verts, int numTris, float extentHint, Bvh &out, std:
     return build_bvh_boxes(boxes.data(), numTris, extentHint, out, err, params);
 }
 
+namespace {
+
+struct Slot {
+    int32_t code;
+    float lo[3], hi[3];
+};
+
+class Collapser {
+public:
+    Collapser(const Bvh &b, Bvh4 &o) : in_(b), out_(o) {}
+
+    void child(int node, int c, Slot &sl) const {
+        const uint32_t *w = &in_.nodes[size_t(node) * kNodeWords];
+        float f[12];
+        std::memcpy(f, w, sizeof(f));
+        for (int a = 0; a < 3; ++a) {
+            sl.lo[a] = f[6 * c + a];
+            sl.hi[a] = f[6 * c + 3 + a];
+        }
+        sl.code = int32_t(w[12 + c]);
+    }
+
+    static float area(const Slot &sl) {
+        const float dx = sl.hi[0] - sl.lo[0], dy = sl.hi[1] - sl.lo[1], dz = sl.hi[2] - sl.lo[2];
+        return 2.0f * (dx * dy + dy * dz + dz * dx);
+    }
+
+    // Emits the 4-wide node for 2-wide node `node` (and its subtree); returns its index.
+    int emit(int node, int pushesAbove, int level) {
+        Slot slots[4];
+        int n = 2;
+        child(node, 0, slots[0]);
+        child(node, 1, slots[1]);
+        while (n < 4) {
+            int best = -1;
+            for (int i = 0; i < n; ++i)
+                if (slots[i].code >= 0 && (best < 0 || area(slots[i]) > area(slots[best]))) best = i;
+            if (best < 0) break;
+            const int open = slots[best].code;
+            child(open, 0, slots[best]);
+            child(open, 1, slots[n++]);
+        }
+        const int idx = int(out_.nodes.size() / kNode4Words);
+        out_.nodes.resize(out_.nodes.size() + kNode4Words, 0u);
+        out_.levels = std::max(out_.levels, level);
+        const int pushes = pushesAbove + (n - 1);
+        out_.stackBound = std::max(out_.stackBound, pushes);
+        int32_t codes[4];
+        for (int i = 0; i < 4; ++i) codes[i] = i < n ? slots[i].code : leaf_code(0, 0);
+        for (int i = 0; i < n; ++i)
+            if (slots[i].code >= 0) codes[i] = emit(slots[i].code, pushes, level + 1);
+        float f[24];
+        for (int i = 0; i < 4; ++i)
+            for (int a = 0; a < 3; ++a) {
+                // unused slot: a point far outside any scene (an empty leaf if ever reached)
+                f[8 * a + i] = i < n ? slots[i].lo[a] : kFar[a];
+                f[8 * a + 4 + i] = i < n ? slots[i].hi[a] : kFar[a];
+            }
+        uint32_t *dst = &out_.nodes[size_t(idx) * kNode4Words];
+        std::memcpy(dst, f, sizeof(f));
+        for (int i = 0; i < 4; ++i) dst[24 + i] = uint32_t(codes[i]);
+        return idx;
+    }
+
+private:
+    static constexpr float kFar[3] = {3.0e38f, -1.0e20f, 7.0e33f};
+    const Bvh &in_;
+    Bvh4 &out_;
+};
+
+}  // namespace
+
+void collapse_bvh4(const Bvh &bvh2, Bvh4 &out) {
+    out.nodes.clear();
+    out.levels = 0;
+    out.stackBound = 0;
+    Collapser(bvh2, out).emit(0, 0, 1);
+}
+
 }  // namespace hippt

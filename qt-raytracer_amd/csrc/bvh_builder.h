@@ -48,4 +48,17 @@ bool build_bvh_boxes(const float *boxes, int numPrims, float extentHint, Bvh &ou
 
 inline int32_t leaf_code(int first, int count) { return ~((first << 4) | count); }
 
+// 4-wide BVH collapsed from a 2-wide one (same leaves, so the same primitive order): each
+// node opens the interior child of largest surface area until it has 4 children.  128-byte
+// nodes, children in SoA: lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] code[4] pad[4];
+// an unused slot holds an empty leaf under a box far outside the scene.
+constexpr int kNode4Words = 32;
+struct Bvh4 {
+    std::vector<uint32_t> nodes;  // kNode4Words per node; node 0 is the root
+    int levels = 0;               // nodes on the deepest root-to-leaf path
+    int stackBound = 0;           // most entries a traversal stack can hold: max over nodes of
+                                  // the (children - 1) pushes of it and its ancestors
+};
+void collapse_bvh4(const Bvh &bvh2, Bvh4 &out);
+
 }  // namespace hippt

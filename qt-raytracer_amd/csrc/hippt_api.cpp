@@ -28,6 +28,7 @@
 
 struct hipptBvh {
     hippt::Bvh bvh;
+    hippt::Bvh4 bvh4;
 };
 
 namespace {
@@ -36,6 +37,9 @@ using hippt::CameraF;
 
 constexpr int kStatWords = 32;  // [0..3] hipptStats counters, [4..19] phase profile
 
+// 4-wide traversal: LDS stack content capacity for scenes outside LDS (19 + 3 spare entries =
+// 22 KB per 256-lane block: 7 blocks per CU in 160 KB).
+constexpr int kWideStackCap = 19;
 constexpr size_t kQueueBytes = 8 * 32 * sizeof(unsigned);  // hippt_trace.h kQueues x kQueueStride
 
 struct EventPair {
@@ -54,6 +58,9 @@ struct Ctx {
     unsigned long long *stats = nullptr;
     int sceneVersion = -1;
     float4 *nodes = nullptr, *tris = nullptr, *shade = nullptr, *mats = nullptr;
+    float4 *nodes4 = nullptr;  // 4-wide BVH (same primitive order as nodes)
+    int *spill = nullptr;      // 4-wide traversal: per-lane stack spill area
+    size_t spillBytes = 0;
     // wavefront path-state pool (allocated on first use)
     void *wfPool = nullptr;
     unsigned wfSlots = 0;
@@ -76,6 +83,8 @@ struct SceneHost {
     int version = 0;
     std::vector<float4> nodes, tris, shade, mats;  // device layouts (hippt_device.h MeshParams)
     int numTris = 0, numNodes = 0, levels = 0;  // numTris: primitive records (triangles + spheres)
+    std::vector<float4> nodes4;                 // 4-wide BVH (bvh_builder.h Bvh4)
+    int numNodes4 = 0, levels4 = 0, stackBound4 = 0;
     bool full = false;                          // spheres or non-Lambertian materials
     double lookfrom[3] = {0, 0, 0}, lookat[3] = {0, 0, -1}, vup[3] = {0, 1, 0};
     double vfov = 90, aperture = 0, focus = 1;
@@ -112,6 +121,9 @@ struct State {
     unsigned chunk = 256;
     int leafExit = -1;  // -1: automatic from the tree depth and LDS residency
     int nodeExit = -1;  // -1: automatic
+    int bvhWidth = 0;   // megakernel traversal over the 2- or 4-wide BVH; 0: 4-wide if it fits in LDS
+    int stackCap = 0;   // 4-wide LDS stack entries (0: automatic)
+    int activeWidth = 0;  // BVH width of the last mesh render (hipptActiveBvhWidth)
     int blocksPerCu = 0;
     bool ldsScene = true;
     int pathMode = 0;             // 0 megakernel, 1 wavefront
@@ -199,7 +211,8 @@ void free_scene_buffers(Ctx &c) {
     (void)hipFree(c.tris);
     (void)hipFree(c.shade);
     (void)hipFree(c.mats);
-    c.nodes = c.tris = c.shade = c.mats = nullptr;
+    (void)hipFree(c.nodes4);
+    c.nodes = c.tris = c.shade = c.mats = c.nodes4 = nullptr;
     c.sceneVersion = -1;
 }
 
@@ -213,6 +226,9 @@ void destroy_ctx(Ctx &c) {
     (void)hipFree(c.stats);
     (void)hipFree(c.wfPool);
     (void)hipFree(c.wfCtr);
+    (void)hipFree(c.spill);
+    c.spill = nullptr;
+    c.spillBytes = 0;
     (void)hipHostFree(c.wfHost);
     for (hipEvent_t e : c.wfPoll)
         if (e) (void)hipEventDestroy(e);
@@ -295,7 +311,7 @@ bool ensure_scene(Ctx &c, const char **err) {
         return true;
     };
     if (!up(c.nodes, s.scene.nodes) || !up(c.tris, s.scene.tris) || !up(c.shade, s.scene.shade) ||
-        !up(c.mats, s.scene.mats))
+        !up(c.mats, s.scene.mats) || !up(c.nodes4, s.scene.nodes4))
         return false;
     c.sceneVersion = s.scene.version;
     return true;
@@ -366,8 +382,8 @@ bool init_locked(int width, int height, const char **err) {
     return false;
 }
 
-long long occupancy_key(int version, int stackDepth, bool lds, bool full) {
-    return ((long long)version << 8) | (stackDepth << 2) | (lds ? 2 : 0) | (full ? 1 : 0);
+long long occupancy_key(int version, int stackDepth, bool lds, bool full, bool wide = false) {
+    return ((long long)version << 9) | (stackDepth << 3) | (wide ? 4 : 0) | (lds ? 2 : 0) | (full ? 1 : 0);
 }
 
 // Wavefront variant (hippt_wavefront.hip): init + generate, then extend/shade/generate
@@ -504,16 +520,31 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                     c.scratchBytes = need;
                 }
                 const bool cnt = s.countTraversal;
-                const int stackDepth = std::max(1, s.scene.levels);
-                const int numNodes = s.scene.numNodes, numTris = s.scene.numTris;
+                // Megakernel traversal over the 4-wide tree (HIPPT_OPT_BVH_WIDTH; wavefront: 2-wide).
+                // Automatic: 4-wide for LDS-resident scenes (Cornell 31.3 -> 32.9 G), 2-wide when the
+                // nodes come from global memory (4-wide measured blob70k -6%, random_scene +-0).
+                const bool fitsLds4 =
+                    s.ldsScene && hippt::mesh_lds_bytes(0, s.scene.numNodes4, s.scene.numTris, true) <=
+                                      hippt::mesh_lds_scene_limit();
+                const bool wide = s.pathMode == 0 && s.scene.numNodes4 > 0 &&
+                                  (s.bvhWidth == 4 || (s.bvhWidth == 0 && fitsLds4));
+                s.activeWidth = wide ? 4 : 2;
+                const int numNodes = wide ? s.scene.numNodes4 : s.scene.numNodes, numTris = s.scene.numTris;
                 // small scenes live in LDS (scene bytes beyond the stack under the limit)
-                const bool ldsScene =
-                    s.ldsScene && hippt::mesh_lds_bytes(0, numNodes, numTris) <= hippt::mesh_lds_scene_limit();
-                const long long occKey = occupancy_key(s.scene.version, stackDepth, ldsScene, s.scene.full);
+                const bool ldsScene = s.ldsScene && hippt::mesh_lds_bytes(0, numNodes, numTris, wide) <=
+                                                        hippt::mesh_lds_scene_limit();
+                // LDS stack entries per lane: 2-wide = interior levels (+1 spare); 4-wide = the
+                // builder's exact bound up to kWideStackCap (+3 spare; deeper stacks spill their
+                // bottom half to global memory), so that 7 blocks of a big scene fit in LDS
+                const int capLimit = s.stackCap > 0 ? s.stackCap : ldsScene ? 30 : kWideStackCap;
+                const int stackCap = wide ? std::max(1, std::min(s.scene.stackBound4, capLimit)) : 0;
+                const int stackDepth = wide ? stackCap + 2 : std::max(1, s.scene.levels);
+                const bool spills = wide && s.scene.stackBound4 > stackCap;
+                const long long occKey = occupancy_key(s.scene.version, stackDepth, ldsScene, s.scene.full, wide);
                 if (c.occKey != occKey) {
                     const int ln = ldsScene ? numNodes : 0, lt = ldsScene ? numTris : 0;
-                    c.meshBlocksPerCu[0] = hippt::mesh_blocks_per_cu(false, s.scene.full, stackDepth, ln, lt);
-                    c.meshBlocksPerCu[1] = hippt::mesh_blocks_per_cu(true, s.scene.full, stackDepth, ln, lt);
+                    c.meshBlocksPerCu[0] = hippt::mesh_blocks_per_cu(false, s.scene.full, wide, stackDepth, ln, lt);
+                    c.meshBlocksPerCu[1] = hippt::mesh_blocks_per_cu(true, s.scene.full, wide, stackDepth, ln, lt);
                     c.occKey = occKey;
                 }
                 int bpc = s.blocksPerCu > 0 ? s.blocksPerCu : c.meshBlocksPerCu[cnt ? 1 : 0];
@@ -525,7 +556,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         HIP_TRY(hipMemsetAsync(c.scratch, 0, size_t(total) * 3 * sizeof(float), c.stream));
                     } else {
                         hippt::MeshParams p{};
-                        p.nodes = c.nodes;
+                        p.nodes = wide ? c.nodes4 : c.nodes;
                         p.tris = c.tris;
                         p.shade = c.shade;
                         p.mats = c.mats;
@@ -559,14 +590,29 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         // 21 levels: 9.8 -> 12.5 G), LDS scenes at 4; every scene leaves the leaf loop
                         // once <= 48 lanes hold a leaf (Cornell 28.4 -> 31.3 G, blob -> 13.4 G).
                         p.leafExit = unsigned(s.leafExit >= 0 ? s.leafExit
-                                                              : ldsScene ? 4 : std::clamp(stackDepth - 6, 0, 16));
+                                                              : ldsScene ? 4 : std::clamp(s.scene.levels - 6, 0, 16));
                         p.nodeExit = unsigned(s.nodeExit >= 0 ? s.nodeExit : 48);
+                        p.wide = wide ? 1 : 0;
+                        p.stackCap = stackCap;
                         if (s.pathMode == 1) {
                             if (!run_wavefront(c, p, cnt, err)) return false;
                         } else {
                             long long blocks = (long long)c.cus * bpc;
                             blocks = std::min<long long>(blocks, (total + hippt::kMeshBlock - 1) / hippt::kMeshBlock);
                             blocks = std::max<long long>(blocks, 1);
+                            if (spills) {
+                                p.spillCap = s.scene.stackBound4 + 3;
+                                const size_t bytes = size_t(blocks) * hippt::kMeshBlock * size_t(p.spillCap) * sizeof(int);
+                                if (c.spillBytes < bytes) {
+                                    HIP_TRY(hipStreamSynchronize(c.stream));
+                                    (void)hipFree(c.spill);
+                                    c.spill = nullptr;
+                                    c.spillBytes = 0;
+                                    HIP_TRY(hipMalloc(&c.spill, bytes));
+                                    c.spillBytes = bytes;
+                                }
+                                p.spill = c.spill;
+                            }
                             HIP_TRY(hipMemsetAsync(c.queue, 0, kQueueBytes, c.stream));
                             EventPair ev;
                             if (!next_events(c, ev, err)) return false;
@@ -714,6 +760,13 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
     SceneHost &sc = s.scene;
     sc.nodes.assign(bvh.nodes.size() / 4, float4{});
     std::memcpy(sc.nodes.data(), bvh.nodes.data(), bvh.nodes.size() * sizeof(uint32_t));
+    hippt::Bvh4 bvh4;
+    hippt::collapse_bvh4(bvh, bvh4);
+    sc.nodes4.assign(bvh4.nodes.size() / 4, float4{});
+    std::memcpy(sc.nodes4.data(), bvh4.nodes.data(), bvh4.nodes.size() * sizeof(uint32_t));
+    sc.numNodes4 = int(bvh4.nodes.size() / hippt::kNode4Words);
+    sc.levels4 = bvh4.levels;
+    sc.stackBound4 = bvh4.stackBound;
     sc.tris.assign(size_t(numPrims) * 3, float4{});
     sc.shade.assign(size_t(numPrims), float4{});
     for (int k = 0; k < numPrims; ++k) {
@@ -1076,8 +1129,21 @@ extern "C" bool hipptSetOption(int key, long long value) {
         if (value != 0 && value != 1) return false;
         s.bvh.sahMode = int(value);
         return true;
+    case HIPPT_OPT_BVH_WIDTH:
+        if (value != 0 && value != 2 && value != 4) return false;
+        s.bvhWidth = int(value);
+        return true;
+    case HIPPT_OPT_STACK_CAP:
+        if (value != 0 && (value < 4 || value > 30)) return false;
+        s.stackCap = int(value);
+        return true;
     default: return false;
     }
+}
+
+extern "C" int hipptActiveBvhWidth(void) {
+    std::lock_guard<std::mutex> g(S().mu);
+    return S().activeWidth;
 }
 
 extern "C" long long hipptGetOption(int key) {
@@ -1099,6 +1165,8 @@ extern "C" long long hipptGetOption(int key) {
     case HIPPT_OPT_LEAF_EXIT: return s.leafExit;
     case HIPPT_OPT_NODE_EXIT: return s.nodeExit;
     case HIPPT_OPT_BVH_SAH: return s.bvh.sahMode;
+    case HIPPT_OPT_BVH_WIDTH: return s.bvhWidth;
+    case HIPPT_OPT_STACK_CAP: return s.stackCap;
     default: return -1;
     }
 }
@@ -1120,6 +1188,7 @@ extern "C" hipptBvh *hipptBvhBuild(const float *verts, int numTris, float extent
         fail(err, msg.empty() ? "null vertex pointer" : msg);
         return nullptr;
     }
+    hippt::collapse_bvh4(b->bvh, b->bvh4);
     return b;
 }
 
@@ -1131,3 +1200,11 @@ extern "C" void hipptBvhCopy(const hipptBvh *b, uint32_t *nodes, int *triOrder) 
     if (triOrder) std::memcpy(triOrder, b->bvh.order.data(), b->bvh.order.size() * sizeof(int));
 }
 extern "C" void hipptBvhFree(hipptBvh *b) { delete b; }
+extern "C" int hipptBvh4NodeCount(const hipptBvh *b) {
+    return b ? int(b->bvh4.nodes.size() / hippt::kNode4Words) : 0;
+}
+extern "C" int hipptBvh4Depth(const hipptBvh *b) { return b ? b->bvh4.levels : 0; }
+extern "C" int hipptBvh4StackBound(const hipptBvh *b) { return b ? b->bvh4.stackBound : 0; }
+extern "C" void hipptBvh4Copy(const hipptBvh *b, uint32_t *nodes) {
+    if (b && nodes) std::memcpy(nodes, b->bvh4.nodes.data(), b->bvh4.nodes.size() * sizeof(uint32_t));
+}

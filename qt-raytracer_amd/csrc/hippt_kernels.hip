@@ -164,6 +164,8 @@ __global__ __launch_bounds__(256) void sphere4_kernel(Sphere4Params P) {
 // 16 distinct 4-bank groups, so ds_read_b128 of different nodes in a lane group do not
 // conflict), primitives at 48 bytes (12 dwords, likewise), shading records at 16 bytes.
 constexpr int kLdsNodeF4 = 5;
+// 4-wide nodes in LDS: the 7 float4 in use (boxes + codes) at a 112-byte stride.
+constexpr int kLdsNode4F4 = 7;
 
 #ifdef HIPPT_DEBUG_TIMELINE
 // per wave: [0] start, [1] first drained fetch, [2] end (s_memrealtime, 100 MHz), [3] items,
@@ -182,8 +184,8 @@ __device__ unsigned long long g_timeline[65536 * 6];
 #endif
 #define HIPPT_SGPR_ATTR __attribute__((amdgpu_num_sgpr(HIPPT_NUM_SGPR)))
 
-template <bool STATS, bool LDS_SCENE, bool FULL>
-__global__ __launch_bounds__(kMeshBlock, FULL ? 7 : HIPPT_MESH_WAVES_PER_EU) HIPPT_SGPR_ATTR void mesh_kernel(MeshParams P) {
+template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE>
+__global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? 7 : HIPPT_MESH_WAVES_PER_EU) HIPPT_SGPR_ATTR void mesh_kernel(MeshParams P) {
 #ifdef HIPPT_DEBUG_TIMELINE
     const unsigned tlw = blockIdx.x * 4u + (threadIdx.x >> 6);
     unsigned long long tlDrained = 0, tlItems = 0;
@@ -200,12 +202,18 @@ __global__ __launch_bounds__(kMeshBlock, FULL ? 7 : HIPPT_MESH_WAVES_PER_EU) HIP
     int *const my = stk + threadIdx.x;
 
     const float4 *nodes = P.nodes, *tris = P.tris, *shade = P.shade;
+    constexpr int ldsNodeF4 = WIDE ? kLdsNode4F4 : kLdsNodeF4;
     if (LDS_SCENE) {
         float4 *sNodes = reinterpret_cast<float4 *>(stk + (P.stackDepth + 1) * kMeshBlock);
-        float4 *sTris = sNodes + P.numNodes * kLdsNodeF4;
+        float4 *sTris = sNodes + P.numNodes * ldsNodeF4;
         float4 *sShade = sTris + P.numTris * 3;
-        for (int i = threadIdx.x; i < P.numNodes * 4; i += kMeshBlock)
-            sNodes[(i >> 2) * kLdsNodeF4 + (i & 3)] = P.nodes[i];
+        if (WIDE) {
+            for (int i = threadIdx.x; i < P.numNodes * kLdsNode4F4; i += kMeshBlock)
+                sNodes[i] = P.nodes[(i / kLdsNode4F4) * 8 + i % kLdsNode4F4];
+        } else {
+            for (int i = threadIdx.x; i < P.numNodes * 4; i += kMeshBlock)
+                sNodes[(i >> 2) * kLdsNodeF4 + (i & 3)] = P.nodes[i];
+        }
         for (int i = threadIdx.x; i < P.numTris * 3; i += kMeshBlock) sTris[i] = P.tris[i];
         for (int i = threadIdx.x; i < P.numTris; i += kMeshBlock) sShade[i] = P.shade[i];
         __syncthreads();
@@ -213,7 +221,8 @@ __global__ __launch_bounds__(kMeshBlock, FULL ? 7 : HIPPT_MESH_WAVES_PER_EU) HIP
         tris = sTris;
         shade = sShade;
     }
-    constexpr int nodeF4 = LDS_SCENE ? kLdsNodeF4 : 4;
+    constexpr int nodeF4 = LDS_SCENE ? ldsNodeF4 : (WIDE ? 8 : 4);
+    const SpillArea S{P.spill, (blockIdx.x * unsigned(kMeshBlock) + threadIdx.x) * unsigned(P.spillCap), P.stackCap};
 
     WorkQueue Q;
     queue_begin(Q, P.totalItems, P.chunk);
@@ -260,7 +269,11 @@ __global__ __launch_bounds__(kMeshBlock, FULL ? 7 : HIPPT_MESH_WAVES_PER_EU) HIP
         // ---- traversal: while-while over the BVH; leave once few lanes remain -------------
         do {
             prof<STATS>(pc, 2);
-            traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
+            if (WIDE)
+                traverse_round_wide<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit,
+                                                         P.nodeExit, S);
+            else
+                traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
         } while (__popcll(__ballot(busy(T))) > unsigned(P.waveThreshold));
 
         // ---- shading: lanes whose traversal finished (ray_color step, RayTracer.h:579-596) ----
@@ -361,9 +374,9 @@ hipError_t launch_sphere4(const Sphere4Params &p, hipStream_t s) {
 
 // Stack: one spare slot per lane above the deepest level for the speculative far-child
 // write; then (LDS_SCENE) the scene copy.
-size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris) {
-    return size_t(stackDepth + 1) * kMeshBlock * sizeof(int) + size_t(ldsNodes) * kLdsNodeF4 * 16 +
-           size_t(ldsTris) * (3 + 1) * 16;
+size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide) {
+    return size_t(stackDepth + 1) * kMeshBlock * sizeof(int) +
+           size_t(ldsNodes) * (wide ? kLdsNode4F4 : kLdsNodeF4) * 16 + size_t(ldsTris) * (3 + 1) * 16;
 }
 
 size_t mesh_lds_scene_limit() { return 24u << 10; }
@@ -373,20 +386,26 @@ size_t mesh_lds_scene_limit() { return 24u << 10; }
 static constexpr int kMaxResidentBlocks = 800 / (HIPPT_NUM_SGPR + 16) < 8 ? 800 / (HIPPT_NUM_SGPR + 16) : 8;
 
 using MeshFn = void (*)(MeshParams);
-static MeshFn mesh_fn(bool count, bool lds, bool full) {
-    if (full) {
-        if (count) return lds ? mesh_kernel<true, true, true> : mesh_kernel<true, false, true>;
-        return lds ? mesh_kernel<false, true, true> : mesh_kernel<false, false, true>;
-    }
-    if (count) return lds ? mesh_kernel<true, true, false> : mesh_kernel<true, false, false>;
-    return lds ? mesh_kernel<false, true, false> : mesh_kernel<false, false, false>;
+template <bool STATS, bool FULL, bool WIDE>
+static MeshFn mesh_fn_lds(bool lds) {
+    return lds ? mesh_kernel<STATS, true, FULL, WIDE> : mesh_kernel<STATS, false, FULL, WIDE>;
+}
+template <bool STATS, bool FULL>
+static MeshFn mesh_fn_wide(bool lds, bool wide) {
+    return wide ? mesh_fn_lds<STATS, FULL, true>(lds) : mesh_fn_lds<STATS, FULL, false>(lds);
+}
+static MeshFn mesh_fn(bool count, bool lds, bool full, bool wide) {
+    if (count) return full ? mesh_fn_wide<true, true>(lds, wide) : mesh_fn_wide<true, false>(lds, wide);
+    return full ? mesh_fn_wide<false, true>(lds, wide) : mesh_fn_wide<false, false>(lds, wide);
 }
 
 hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hipStream_t s) {
     if (p.stackDepth < 1 || p.stackDepth > kStackDepth) return hipErrorInvalidValue;
+    if (p.wide && (p.stackCap < 1 || p.stackCap + 2 > p.stackDepth)) return hipErrorInvalidValue;
     const bool lds = p.ldsScene != 0;
-    const size_t bytes = mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0);
-    hipLaunchKernelGGL(mesh_fn(countTraversal, lds, p.full != 0), dim3(blocks), dim3(kMeshBlock), bytes, s, p);
+    const size_t bytes = mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0, p.wide != 0);
+    hipLaunchKernelGGL(mesh_fn(countTraversal, lds, p.full != 0, p.wide != 0), dim3(blocks), dim3(kMeshBlock), bytes,
+                       s, p);
     return hipGetLastError();
 }
 
@@ -398,12 +417,12 @@ hipError_t launch_combine(const CombineParams &p, hipStream_t s) {
     return hipGetLastError();
 }
 
-int mesh_blocks_per_cu(bool countTraversal, bool full, int stackDepth, int ldsNodes, int ldsTris) {
+int mesh_blocks_per_cu(bool countTraversal, bool full, bool wide, int stackDepth, int ldsNodes, int ldsTris) {
     int n = 0;
     const bool lds = ldsNodes > 0;
-    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris);
-    hipError_t e =
-        hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mesh_fn(countTraversal, lds, full), kMeshBlock, bytes);
+    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, wide);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mesh_fn(countTraversal, lds, full, wide),
+                                                                kMeshBlock, bytes);
     if (e != hipSuccess || n <= 0) n = 1;
     // the query ignores the trap handler's SGPRs (kMaxResidentBlocks): a larger persistent grid
     // leaves blocks waiting for a slot until others finish

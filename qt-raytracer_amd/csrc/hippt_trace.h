@@ -381,6 +381,7 @@ struct Trav {
     int leaf;   // postponed leaf code or 0
     float bestT;
     int bestI, bestO;
+    int ovf;    // 4-wide BVH: entries moved to the lane's spill area (bottom of its stack)
 };
 
 // Traversal still has work: nodes to visit or a postponed leaf to test.
@@ -389,10 +390,60 @@ __device__ __forceinline__ bool busy(const Trav &T) { return T.cur != kDone || T
 __device__ __forceinline__ void begin(Trav &T) {
     T.cur = 0;
     T.sp = 0;
+    T.ovf = 0;
     T.leaf = 0;
     T.bestT = INFINITY;
     T.bestI = -1;
     T.bestO = 0x7fffffff;
+}
+
+// The primitives of leaf T.leaf against the ray: closest hit = min (t, primitive id).
+template <bool STATS, bool FULL>
+__device__ __forceinline__ void test_leaf(Trav &T, const Ray &r, const float4 *tris, unsigned long long &ntest,
+                                          unsigned *pc) {
+    const float tmin = 0.001f;
+    const int code = ~T.leaf;
+    const int first = code >> 4, last = first + (code & 15);
+    for (int i = first; i < last; ++i) {
+        const float4 *tp = tris + 3 * i;
+        const float4 A = tp[0], B = tp[1], Cc = tp[2];
+        prof<STATS>(pc, 5);
+        if (STATS) ++ntest;
+        if (FULL && __float_as_int(Cc.z) != 0) {
+            float tt;
+            const int orig = __float_as_int(Cc.y);
+            if (sphere_t(A, B.x, r, tmin, tt) && (tt < T.bestT || (tt == T.bestT && orig < T.bestO))) {
+                T.bestT = tt;
+                T.bestI = i;
+                T.bestO = orig;
+            }
+            continue;
+        }
+        // Möller–Trumbore, division-free edge tests (pt_oracle.c po_tri_hit)
+        const float e1x = A.w, e1y = B.x, e1z = B.y;
+        const float e2x = B.z, e2y = B.w, e2z = Cc.x;
+        const float pvx = fmaf(r.dy, e2z, -(r.dz * e2y));
+        const float pvy = fmaf(r.dz, e2x, -(r.dx * e2z));
+        const float pvz = fmaf(r.dx, e2y, -(r.dy * e2x));
+        const float det = fdot(e1x, e1y, e1z, pvx, pvy, pvz);
+        const float tvx = r.ox - A.x, tvy = r.oy - A.y, tvz = r.oz - A.z;
+        const float un = fdot(tvx, tvy, tvz, pvx, pvy, pvz);
+        const float qvx = fmaf(tvy, e1z, -(tvz * e1y));
+        const float qvy = fmaf(tvz, e1x, -(tvx * e1z));
+        const float qvz = fmaf(tvx, e1y, -(tvy * e1x));
+        const float vn = fdot(r.dx, r.dy, r.dz, qvx, qvy, qvz);
+        const bool neg = det < 0.0f;
+        const float us = neg ? -un : un, vs = neg ? -vn : vn;
+        if (det != 0.0f && us >= 0.0f && vs >= 0.0f && us + vs <= fabsf(det)) {
+            const float tt = fdot(e2x, e2y, e2z, qvx, qvy, qvz) / det;
+            const int orig = __float_as_int(Cc.y);
+            if (tt >= tmin && (tt < T.bestT || (tt == T.bestT && orig < T.bestO))) {
+                T.bestT = tt;
+                T.bestI = i;
+                T.bestO = orig;
+            }
+        }
+    }
 }
 
 // One speculative while-while round (Aila & Laine 2009) over the BVH: interior loop until
@@ -444,48 +495,7 @@ __device__ __forceinline__ void traverse_round(Trav &T, const Ray &r, int *my, c
     }
     while (T.leaf != 0) {
         prof<STATS>(pc, 4);
-        const int code = ~T.leaf;
-        const int first = code >> 4, last = first + (code & 15);
-        for (int i = first; i < last; ++i) {
-            const float4 *tp = tris + 3 * i;
-            const float4 A = tp[0], B = tp[1], Cc = tp[2];
-            prof<STATS>(pc, 5);
-            if (STATS) ++ntest;
-            if (FULL && __float_as_int(Cc.z) != 0) {
-                float tt;
-                const int orig = __float_as_int(Cc.y);
-                if (sphere_t(A, B.x, r, tmin, tt) && (tt < T.bestT || (tt == T.bestT && orig < T.bestO))) {
-                    T.bestT = tt;
-                    T.bestI = i;
-                    T.bestO = orig;
-                }
-                continue;
-            }
-            // Möller–Trumbore, division-free edge tests (pt_oracle.c po_tri_hit)
-            const float e1x = A.w, e1y = B.x, e1z = B.y;
-            const float e2x = B.z, e2y = B.w, e2z = Cc.x;
-            const float pvx = fmaf(r.dy, e2z, -(r.dz * e2y));
-            const float pvy = fmaf(r.dz, e2x, -(r.dx * e2z));
-            const float pvz = fmaf(r.dx, e2y, -(r.dy * e2x));
-            const float det = fdot(e1x, e1y, e1z, pvx, pvy, pvz);
-            const float tvx = r.ox - A.x, tvy = r.oy - A.y, tvz = r.oz - A.z;
-            const float un = fdot(tvx, tvy, tvz, pvx, pvy, pvz);
-            const float qvx = fmaf(tvy, e1z, -(tvz * e1y));
-            const float qvy = fmaf(tvz, e1x, -(tvx * e1z));
-            const float qvz = fmaf(tvx, e1y, -(tvy * e1x));
-            const float vn = fdot(r.dx, r.dy, r.dz, qvx, qvy, qvz);
-            const bool neg = det < 0.0f;
-            const float us = neg ? -un : un, vs = neg ? -vn : vn;
-            if (det != 0.0f && us >= 0.0f && vs >= 0.0f && us + vs <= fabsf(det)) {
-                const float tt = fdot(e2x, e2y, e2z, qvx, qvy, qvz) / det;
-                const int orig = __float_as_int(Cc.y);
-                if (tt >= tmin && (tt < T.bestT || (tt == T.bestT && orig < T.bestO))) {
-                    T.bestT = tt;
-                    T.bestI = i;
-                    T.bestO = orig;
-                }
-            }
-        }
+        test_leaf<STATS, FULL>(T, r, tris, ntest, pc);
         // a leaf that was next in line is processed in the same loop
         T.leaf = 0;
         if (T.cur < 0 && T.cur != kDone) {
@@ -493,6 +503,114 @@ __device__ __forceinline__ void traverse_round(Trav &T, const Ray &r, int *my, c
             T.cur = T.sp > 0 ? my[T.sp -= kMeshBlock] : kDone;
         }
         // back to the node loop once at most nodeExit lanes still hold a leaf (they keep it)
+        if (nodeExit && __popcll(__ballot(T.leaf != 0)) <= nodeExit) break;
+    }
+}
+
+// ---- 4-wide BVH (bvh_builder.h Bvh4) ------------------------------------------------------
+// Stack: entries in LDS (`cap` of them; 3 spare slots above for the unconditional writes), the
+// bottom of a deeper stack in the lane's global spill area (spill[base ...], rare: the builder's
+// exact bound exceeds `cap` only for deep trees, and real rays stay far below the bound).
+struct SpillArea {
+    int *buf;
+    unsigned base;  // this lane's first entry
+    int cap;        // LDS entries in use at most (the stack content capacity)
+};
+
+__device__ __forceinline__ void spill_bottom(Trav &T, int *my, const SpillArea &S) {
+    const int half = S.cap >> 1, n = T.sp / kMeshBlock;
+    for (int j = 0; j < half; ++j) S.buf[S.base + unsigned(T.ovf + j)] = my[j * kMeshBlock];
+    for (int j = half; j < n; ++j) my[(j - half) * kMeshBlock] = my[j * kMeshBlock];
+    T.sp -= half * kMeshBlock;
+    T.ovf += half;
+}
+
+__device__ __forceinline__ void refill_bottom(Trav &T, int *my, const SpillArea &S) {
+    const int n = min(S.cap >> 1, T.ovf);
+    T.ovf -= n;
+    for (int j = 0; j < n; ++j) my[j * kMeshBlock] = S.buf[S.base + unsigned(T.ovf + j)];
+    T.sp = n * kMeshBlock;
+}
+
+__device__ __forceinline__ int pop_wide(Trav &T, int *my, const SpillArea &S) {
+    if (T.sp == 0 && T.ovf != 0) refill_bottom(T, my, S);
+    if (T.sp == 0) return kDone;
+    T.sp -= kMeshBlock;
+    return my[T.sp];
+}
+
+// Sort key of a child box: entry distance bits (>= tmin > 0, so ordered as unsigned); a
+// miss sorts last.
+__device__ __forceinline__ unsigned child_key(float lox, float hix, float loy, float hiy, float loz, float hiz,
+                                              const Ray &r, float tmin, float bestT) {
+    const float ax = fmaf(lox, r.ix, -r.oix), bx = fmaf(hix, r.ix, -r.oix);
+    const float ay = fmaf(loy, r.iy, -r.oiy), by = fmaf(hiy, r.iy, -r.oiy);
+    const float az = fmaf(loz, r.iz, -r.oiz), bz = fmaf(hiz, r.iz, -r.oiz);
+    const float n = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
+    const float f = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), bestT));
+    return n <= f ? __float_as_uint(n) : 0xffffffffu;
+}
+
+// Compare-exchange of (key, child code) pairs: afterwards ka <= kb.
+__device__ __forceinline__ void cas(unsigned &ka, int &ca, unsigned &kb, int &cb) {
+    const bool sw = kb < ka;
+    const unsigned k = ka;
+    const int c = ca;
+    ka = sw ? kb : ka;
+    kb = sw ? k : kb;
+    ca = sw ? cb : ca;
+    cb = sw ? c : cb;
+}
+
+// traverse_round over the 4-wide tree: a node visit tests its four child boxes, descends into
+// the nearest hit child and pushes the other hit children far to near.
+template <int NODE_F4, bool STATS, bool FULL>
+__device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *my, const float4 *nodes,
+                                                    const float4 *tris, unsigned long long &nvis,
+                                                    unsigned long long &ntest, unsigned *pc, unsigned leafExit,
+                                                    unsigned nodeExit, const SpillArea &S) {
+    const float tmin = 0.001f;
+    while (T.cur >= 0) {
+        prof<STATS>(pc, 3);
+        const float4 *nd = nodes + __umul24(unsigned(T.cur), unsigned(NODE_F4));
+        const float4 lx = nd[0], hx = nd[1], ly = nd[2], hy = nd[3], lz = nd[4], hz = nd[5];
+        const int4 ch = *reinterpret_cast<const int4 *>(nd + 6);
+        if (STATS) ++nvis;
+        unsigned k0 = child_key(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, r, tmin, T.bestT);
+        unsigned k1 = child_key(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, r, tmin, T.bestT);
+        unsigned k2 = child_key(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, r, tmin, T.bestT);
+        unsigned k3 = child_key(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, tmin, T.bestT);
+        const int nh = int(k0 != 0xffffffffu) + int(k1 != 0xffffffffu) + int(k2 != 0xffffffffu) +
+                       int(k3 != 0xffffffffu);
+        // sorting network (0,1)(2,3)(0,2)(1,3)(1,2), codes carried along: c0 nearest
+        int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
+        cas(k0, c0, k1, c1);
+        cas(k2, c2, k3, c3);
+        cas(k0, c0, k2, c2);
+        cas(k1, c1, k3, c3);
+        cas(k1, c1, k2, c2);
+        if (T.sp + (nh - 1) * kMeshBlock > S.cap * kMeshBlock) spill_bottom(T, my, S);
+        // push c[nh-1] .. c1 (c1 on top); unused writes land in the spare slots above
+        my[T.sp] = nh == 4 ? c3 : (nh == 3 ? c2 : c1);
+        my[T.sp + kMeshBlock] = nh == 4 ? c2 : c1;
+        my[T.sp + 2 * kMeshBlock] = c1;
+        T.sp += nh > 1 ? (nh - 1) * kMeshBlock : 0;
+        T.cur = nh > 0 ? c0 : pop_wide(T, my, S);
+        // postpone the first leaf reached and keep descending
+        if (T.cur < 0 && T.cur != kDone && T.leaf == 0) {
+            T.leaf = T.cur;
+            T.cur = pop_wide(T, my, S);
+        }
+        if (__popcll(__ballot(T.leaf == 0 && T.cur >= 0)) <= leafExit) break;
+    }
+    while (T.leaf != 0) {
+        prof<STATS>(pc, 4);
+        test_leaf<STATS, FULL>(T, r, tris, ntest, pc);
+        T.leaf = 0;
+        if (T.cur < 0 && T.cur != kDone) {
+            T.leaf = T.cur;
+            T.cur = pop_wide(T, my, S);
+        }
         if (nodeExit && __popcll(__ballot(T.leaf != 0)) <= nodeExit) break;
     }
 }

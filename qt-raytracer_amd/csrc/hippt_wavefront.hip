@@ -304,7 +304,7 @@ hipError_t wf_launch_generate(const WfParams &W, int nxt, bool countSamples, hip
 hipError_t wf_launch_extend(const WfParams &W, int cur, int blocks, bool countTraversal, hipStream_t s) {
     const MeshParams &P = W.mp;
     const bool lds = P.ldsScene != 0;
-    const size_t bytes = mesh_lds_bytes(P.stackDepth, lds ? P.numNodes : 0, lds ? P.numTris : 0);
+    const size_t bytes = mesh_lds_bytes(P.stackDepth, lds ? P.numNodes : 0, lds ? P.numTris : 0, false);
     hipLaunchKernelGGL(ext_fn(countTraversal, lds, P.full != 0), dim3(blocks), dim3(kMeshBlock), bytes, s, W, cur);
     return hipGetLastError();
 }
@@ -316,7 +316,7 @@ hipError_t wf_launch_shade(const WfParams &W, int cur, hipStream_t s) {
 
 int wf_extend_blocks_per_cu(bool countTraversal, bool full, int stackDepth, int ldsNodes, int ldsTris) {
     int n = 0;
-    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris);
+    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, false);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ext_fn(countTraversal, ldsNodes > 0, full), kMeshBlock, bytes) !=
             hipSuccess ||
         n <= 0)

@@ -41,6 +41,8 @@ OPT_DEVICE_ROWS = 13
 OPT_LEAF_EXIT = 14
 OPT_NODE_EXIT = 15
 OPT_BVH_SAH = 16
+OPT_BVH_WIDTH = 17
+OPT_STACK_CAP = 18
 
 # Every symbol include/hippt.h declares (checked by tests/test_abi_cpu.py).
 EXPORTS = (
@@ -54,6 +56,7 @@ EXPORTS = (
     "hipptResetAccumulation", "hipptGetStats", "hipptResetStats", "hipptGetCounters", "hipptSetOption",
     "hipptGetOption",
     "hipptLastError", "hipptBvhBuild", "hipptBvhNodeCount", "hipptBvhDepth", "hipptBvhCopy", "hipptBvhFree",
+    "hipptBvh4NodeCount", "hipptBvh4Depth", "hipptBvh4StackBound", "hipptBvh4Copy", "hipptActiveBvhWidth",
 )
 
 
@@ -153,6 +156,11 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     sig("hipptBvhDepth", c_int, ctypes.c_void_p)
     sig("hipptBvhCopy", None, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32), p_int)
     sig("hipptBvhFree", None, ctypes.c_void_p)
+    sig("hipptActiveBvhWidth", c_int)
+    sig("hipptBvh4NodeCount", c_int, ctypes.c_void_p)
+    sig("hipptBvh4Depth", c_int, ctypes.c_void_p)
+    sig("hipptBvh4StackBound", c_int, ctypes.c_void_p)
+    sig("hipptBvh4Copy", None, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32))
     _lib = lib
     return lib
 
@@ -195,7 +203,8 @@ def build_camera(lookfrom, lookat, vup, vfov, aspect, aperture, focus) -> Camera
 
 
 class Bvh:
-    """Host BVH built by libhippt (hipptBvhBuild): nodes (N,16) uint32 and triangle order."""
+    """Host BVH built by libhippt (hipptBvhBuild): nodes (N,16) uint32 and triangle order; the
+    4-wide tree collapsed from it: nodes4 (M,32) uint32, depth4, stack_bound4."""
 
     def __init__(self, verts: np.ndarray, extent_hint: float = 0.0):
         lib = load_library()
@@ -210,6 +219,10 @@ class Bvh:
             self.nodes = np.zeros((n, 16), dtype=np.uint32)
             self.order = np.zeros(v.shape[0], dtype=np.int32)
             lib.hipptBvhCopy(h, _ptr(self.nodes, ctypes.c_uint32), _ptr(self.order, ctypes.c_int))
+            self.depth4 = lib.hipptBvh4Depth(h)
+            self.stack_bound4 = lib.hipptBvh4StackBound(h)
+            self.nodes4 = np.zeros((lib.hipptBvh4NodeCount(h), 32), dtype=np.uint32)
+            lib.hipptBvh4Copy(h, _ptr(self.nodes4, ctypes.c_uint32))
         finally:
             lib.hipptBvhFree(h)
 

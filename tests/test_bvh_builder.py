@@ -100,3 +100,54 @@ def test_bvh_traversal_equals_brute_force(name, w, h):
     a = brute.frames(0, 2, 8)
     b = bvh.frames(0, 2, 8)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2] == b[2]
+
+
+def _decode4(nodes4):
+    f = nodes4[:, :24].view(np.float32).reshape(-1, 3, 2, 4)  # node, axis, lo/hi, slot
+    kids = nodes4[:, 24:28].view(np.int32)
+    return f, kids
+
+
+@pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene"])
+def test_bvh4_collapse_keeps_leaves_and_bounds_subtrees(name):
+    """The 4-wide tree (hipptBvh4*) holds exactly the 2-wide tree's leaves, every child box
+    contains its subtree's primitives, and the stack bound is the max over nodes of the
+    (children - 1) pushes along the path."""
+    sc = scenes.get_scene(name)
+    if sc.num_tris == 0:
+        pytest.skip("sphere-only scene: triangles are the collapse's test subject")
+    bvh = hippt.Bvh(sc.verts, extent_hint=800.0)
+    leaves2 = sorted(tuple(x[:2]) for x in _walk(bvh.nodes)[0])
+    f, kids = _decode4(bvh.nodes4)
+    assert kids.shape[0] >= 1 and bvh.depth4 <= bvh.depth
+    leaves4, bound, depth = [], 0, 0
+    stack = [(0, 0, 1)]
+    seen = np.zeros(len(kids), bool)
+    while stack:
+        n, pushes, d = stack.pop()
+        assert not seen[n]
+        seen[n] = True
+        depth = max(depth, d)
+        used = [c for c in range(4) if not (kids[n, c] == -1 and f[n, 0, 0, c] > 1e37)]
+        assert 2 <= len(used) <= 4
+        bound = max(bound, pushes + len(used) - 1)
+        for c in range(4):
+            k = int(kids[n, c])
+            lo, hi = f[n, :, 0, c], f[n, :, 1, c]
+            if c not in used:  # unused slot: empty leaf under a point far outside the scene
+                assert k == -1 and np.all(lo == hi) and abs(lo[0]) > 1e37
+                continue
+            if k >= 0:
+                # a child node's boxes lie inside this box (the 2-wide boxes it was made of)
+                cu = [cc for cc in range(4) if not (kids[k, cc] == -1 and f[k, 0, 0, cc] > 1e37)]
+                assert np.all(f[k, :, 0, cu].T >= lo[:, None] - 1e-3) and np.all(f[k, :, 1, cu].T <= hi[:, None] + 1e-3)
+                stack.append((k, pushes + len(used) - 1, d + 1))
+            else:
+                code = ~k
+                first, count = code >> 4, code & 15
+                leaves4.append((first, count))
+                v = sc.verts[bvh.order[first:first + count]].reshape(-1, 3)
+                assert np.all(v >= lo) and np.all(v <= hi)
+    assert seen.all()
+    assert sorted(leaves4) == leaves2
+    assert bound == bvh.stack_bound4 and depth == bvh.depth4

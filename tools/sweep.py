@@ -25,7 +25,8 @@ KEYS = {"wave": hippt.OPT_WAVE_THRESHOLD, "chunk": hippt.OPT_CHUNK, "scratch": h
         "bpc": hippt.OPT_BLOCKS_PER_CU, "lds": hippt.OPT_LDS_SCENE, "mode": hippt.OPT_PATH_MODE,
         "slots": hippt.OPT_WAVEFRONT_SLOTS, "leaf": hippt.OPT_BVH_LEAF, "tcost": hippt.OPT_BVH_TRAVERSAL_COST,
         "depth": hippt.OPT_BVH_MAX_DEPTH, "leafexit": hippt.OPT_LEAF_EXIT,
-        "nodeexit": hippt.OPT_NODE_EXIT, "sah": hippt.OPT_BVH_SAH}
+        "nodeexit": hippt.OPT_NODE_EXIT, "sah": hippt.OPT_BVH_SAH,
+        "width": hippt.OPT_BVH_WIDTH, "stackcap": hippt.OPT_STACK_CAP}
 REUPLOAD = {"leaf", "tcost", "depth", "sah"}  # build parameters: take effect at the next upload
 
 
