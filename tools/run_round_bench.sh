@@ -1,12 +1,15 @@
+# tools/run_round_bench.sh TAG — run ON THE GPU BOX (via gpurun): the bench lines of every
+# BASELINE config plus the rocprof profiles of the two headline scenes, into gpurun_out/TAG/.
 set -e
-mkdir -p gpurun_out/r1d
+TAG=${1:?tag}
+mkdir -p gpurun_out/$TAG
 B="timeout -k 10 300 python3 bench.py"
-$B > gpurun_out/r1d/cornell.json 2> gpurun_out/r1d/cornell.err
-$B --scene blob70k --cpu-baseline off > gpurun_out/r1d/blob.json 2>> gpurun_out/r1d/err
-$B --scene blob70k --width 3840 --height 2160 --spp 256 --steps 2 --warmup 1 --cpu-baseline off > gpurun_out/r1d/blob4k.json 2>> gpurun_out/r1d/err
-$B --scene blob70k --path-mode wavefront --cpu-baseline off > gpurun_out/r1d/blob_wf.json 2>> gpurun_out/r1d/err
-$B --scene random_scene --cpu-baseline off > gpurun_out/r1d/random.json 2>> gpurun_out/r1d/err
-$B --scene cornell_mixed --cpu-baseline off > gpurun_out/r1d/mixed.json 2>> gpurun_out/r1d/err
-bash tools/profile.sh r1d
-bash tools/profile.sh r1d_blob --scene blob70k
+$B > gpurun_out/$TAG/cornell.json 2> gpurun_out/$TAG/cornell.err
+$B --scene blob70k --cpu-baseline off > gpurun_out/$TAG/blob.json 2>> gpurun_out/$TAG/err
+$B --scene blob70k --width 3840 --height 2160 --spp 256 --steps 2 --warmup 1 --cpu-baseline off > gpurun_out/$TAG/blob4k.json 2>> gpurun_out/$TAG/err
+$B --scene blob70k --path-mode wavefront --cpu-baseline off > gpurun_out/$TAG/blob_wf.json 2>> gpurun_out/$TAG/err
+$B --scene random_scene --cpu-baseline off > gpurun_out/$TAG/random.json 2>> gpurun_out/$TAG/err
+$B --scene cornell_mixed --cpu-baseline off > gpurun_out/$TAG/mixed.json 2>> gpurun_out/$TAG/err
+bash tools/profile.sh $TAG
+bash tools/profile.sh ${TAG}_blob --scene blob70k
 echo ALLDONE
