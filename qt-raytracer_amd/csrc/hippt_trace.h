@@ -34,6 +34,13 @@ __device__ __forceinline__ float rand01(uint32_t &s) {  // :32-35 (÷4294967295.
     return float(s) * 0x1p-32f;
 }
 
+// 2*rand01 - 1 (fmaf(2, u, -1) of the contract) in one FMA: u = float(s)*2^-32 is an exact
+// power-of-two scaling, so fmaf(float(s), 2^-31, -1) rounds the same exact value 2u - 1.
+__device__ __forceinline__ float rand_pm1(uint32_t &s) {
+    s = hash32(s);
+    return fmaf(float(s), 0x1p-31f, -1.0f);
+}
+
 // Short-cycle escape of the rejection loops (pt_oracle.c PO_ESCAPE).
 __device__ __forceinline__ void escape_cycle(uint32_t &s, unsigned tries) {
     if ((tries & 63u) == 0u) s ^= 0x9E3779B9u;
@@ -214,8 +221,8 @@ __device__ __forceinline__ void camera_sample(const MeshParams &P, unsigned it, 
     const float t = (float(y) + rand01(rng)) * P.invH;
     float qx, qy;
     for (unsigned tries = 1;; ++tries) {  // random_in_unit_disk, RayTracer.h:163-169
-        qx = fmaf(2.0f, rand01(rng), -1.0f);
-        qy = fmaf(2.0f, rand01(rng), -1.0f);
+        qx = rand_pm1(rng);
+        qy = rand_pm1(rng);
         if (fmaf(qx, qx, qy * qy) < 1.0f) break;
         escape_cycle(rng, tries);
     }
@@ -248,9 +255,9 @@ __device__ __forceinline__ float rius(uint32_t &rng, float &rx, float &ry, float
     float r2;
     for (unsigned tries = 1;; ++tries) {
         prof<STATS>(pc, 7);
-        rx = fmaf(2.0f, rand01(rng), -1.0f);
-        ry = fmaf(2.0f, rand01(rng), -1.0f);
-        rz = fmaf(2.0f, rand01(rng), -1.0f);
+        rx = rand_pm1(rng);
+        ry = rand_pm1(rng);
+        rz = rand_pm1(rng);
         r2 = fmaf(rx, rx, fmaf(ry, ry, rz * rz));
         if (r2 < 1.0f) break;
         escape_cycle(rng, tries);
@@ -539,17 +546,23 @@ __device__ __forceinline__ int pop_wide(Trav &T, int *my, const SpillArea &S) {
     return my[T.sp];
 }
 
-// Sort key of a child box: entry distance bits (>= tmin > 0, so ordered as unsigned); a
-// miss sorts last.
-__device__ __forceinline__ unsigned child_key(float lox, float hix, float loy, float hiy, float loz, float hiz,
+// Sort key of a child box from its near and far planes on each axis (the ray's direction signs
+// choose them, see traverse_round_wide): entry distance bits (>= tmin > 0, so ordered as
+// unsigned); a miss sorts last.  Two min/max per bound instead of five: the planes need no
+// min/max ordering.
+__device__ __forceinline__ unsigned child_key(float nx, float fx, float ny, float fy, float nz, float fz,
                                               const Ray &r, float tmin, float bestT) {
-    const float ax = fmaf(lox, r.ix, -r.oix), bx = fmaf(hix, r.ix, -r.oix);
-    const float ay = fmaf(loy, r.iy, -r.oiy), by = fmaf(hiy, r.iy, -r.oiy);
-    const float az = fmaf(loz, r.iz, -r.oiz), bz = fmaf(hiz, r.iz, -r.oiz);
-    const float n = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz), tmin));
-    const float f = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fminf(fmaxf(az, bz), bestT));
+    const float ax = fmaf(nx, r.ix, -r.oix), bx = fmaf(fx, r.ix, -r.oix);
+    const float ay = fmaf(ny, r.iy, -r.oiy), by = fmaf(fy, r.iy, -r.oiy);
+    const float az = fmaf(nz, r.iz, -r.oiz), bz = fmaf(fz, r.iz, -r.oiz);
+    const float n = fmaxf(fmaxf(ax, ay), fmaxf(az, tmin));
+    const float f = fminf(fminf(bx, by), fminf(bz, bestT));
     return n <= f ? __float_as_uint(n) : 0xffffffffu;
 }
+
+// Byte offset of the near-plane row within a (lo, hi) row pair: 16 when the axis's reciprocal
+// direction is negative (its hi plane is entered first), else 0.
+__device__ __forceinline__ int near_row(float inv) { return int((__float_as_uint(inv) >> 27) & 16u); }
 
 // Compare-exchange of (key, child code) pairs: afterwards ka <= kb.
 __device__ __forceinline__ void cas(unsigned &ka, int &ca, unsigned &kb, int &cb) {
@@ -570,16 +583,24 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
                                                     unsigned long long &ntest, unsigned *pc, unsigned leafExit,
                                                     unsigned nodeExit, const SpillArea &S) {
     const float tmin = 0.001f;
+    const int sx = near_row(r.ix), sy = near_row(r.iy), sz = near_row(r.iz);
     while (T.cur >= 0) {
         prof<STATS>(pc, 3);
         const float4 *nd = nodes + __umul24(unsigned(T.cur), unsigned(NODE_F4));
-        const float4 lx = nd[0], hx = nd[1], ly = nd[2], hy = nd[3], lz = nd[4], hz = nd[5];
+        // rows lo.x hi.x lo.y hi.y lo.z hi.z: read as near/far rows of this ray's octant
+        const char *nb = reinterpret_cast<const char *>(nd);
+        const float4 nx = *reinterpret_cast<const float4 *>(nb + sx);
+        const float4 fx = *reinterpret_cast<const float4 *>(nb - sx + 16);
+        const float4 ny = *reinterpret_cast<const float4 *>(nb + sy + 32);
+        const float4 fy = *reinterpret_cast<const float4 *>(nb - sy + 48);
+        const float4 nz = *reinterpret_cast<const float4 *>(nb + sz + 64);
+        const float4 fz = *reinterpret_cast<const float4 *>(nb - sz + 80);
         const int4 ch = *reinterpret_cast<const int4 *>(nd + 6);
         if (STATS) ++nvis;
-        unsigned k0 = child_key(lx.x, hx.x, ly.x, hy.x, lz.x, hz.x, r, tmin, T.bestT);
-        unsigned k1 = child_key(lx.y, hx.y, ly.y, hy.y, lz.y, hz.y, r, tmin, T.bestT);
-        unsigned k2 = child_key(lx.z, hx.z, ly.z, hy.z, lz.z, hz.z, r, tmin, T.bestT);
-        unsigned k3 = child_key(lx.w, hx.w, ly.w, hy.w, lz.w, hz.w, r, tmin, T.bestT);
+        unsigned k0 = child_key(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, r, tmin, T.bestT);
+        unsigned k1 = child_key(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, r, tmin, T.bestT);
+        unsigned k2 = child_key(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z, r, tmin, T.bestT);
+        unsigned k3 = child_key(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w, r, tmin, T.bestT);
         const int nh = int(k0 != 0xffffffffu) + int(k1 != 0xffffffffu) + int(k2 != 0xffffffffu) +
                        int(k3 != 0xffffffffu);
         // sorting network (0,1)(2,3)(0,2)(1,3)(1,2), codes carried along: c0 nearest
