@@ -71,6 +71,8 @@ def parse():
     p.add_argument("--wave-threshold", type=int, default=None)
     p.add_argument("--chunk", type=int, default=None)
     p.add_argument("--scratch-mb", type=int, default=None)
+    p.add_argument("--bvh-width", type=int, default=None, choices=[0, 2, 4],
+                   help="megakernel BVH width (HIPPT_OPT_BVH_WIDTH; default automatic)")
     p.add_argument("--cpu-baseline", default="auto", choices=["auto", "reference", "port", "off"])
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU sample duration")
     p.add_argument("--cpu-threads", type=int, default=None)
@@ -196,6 +198,8 @@ def main():
         pt.setOption(hippt.OPT_CHUNK, args.chunk)
     if args.scratch_mb is not None:
         pt.setOption(hippt.OPT_SCRATCH_MB, args.scratch_mb)
+    if args.bvh_width is not None:
+        pt.setOption(hippt.OPT_BVH_WIDTH, args.bvh_width)
     pt.setOption(hippt.OPT_PATH_MODE, 1 if args.path_mode == "wavefront" else 0)
     if args.wavefront_slots is not None:
         pt.setOption(hippt.OPT_WAVEFRONT_SLOTS, args.wavefront_slots)

@@ -521,13 +521,11 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 }
                 const bool cnt = s.countTraversal;
                 // Megakernel traversal over the 4-wide tree (HIPPT_OPT_BVH_WIDTH; wavefront: 2-wide).
-                // Automatic: 4-wide for LDS-resident scenes (Cornell 31.3 -> 32.9 G), 2-wide when the
-                // nodes come from global memory (4-wide measured blob70k -6%, random_scene +-0).
-                const bool fitsLds4 =
-                    s.ldsScene && hippt::mesh_lds_bytes(0, s.scene.numNodes4, s.scene.numTris, true) <=
-                                      hippt::mesh_lds_scene_limit();
-                const bool wide = s.pathMode == 0 && s.scene.numNodes4 > 0 &&
-                                  (s.bvhWidth == 4 || (s.bvhWidth == 0 && fitsLds4));
+                // Automatic: 4-wide.  With near/far rows read by the ray's octant, 4-wide beats
+                // 2-wide on LDS scenes (Cornell 31.7 -> 35.3 G) and on global-memory trees (blob70k
+                // 14.2 -> 15.4 G: half the dependent node fetches, 18% fewer load instructions);
+                // random_scene (spheres, general kernel) 20.6 vs 20.5 G.
+                const bool wide = s.pathMode == 0 && s.scene.numNodes4 > 0 && s.bvhWidth != 2;
                 s.activeWidth = wide ? 4 : 2;
                 const int numNodes = wide ? s.scene.numNodes4 : s.scene.numNodes, numTris = s.scene.numTris;
                 // small scenes live in LDS (scene bytes beyond the stack under the limit)

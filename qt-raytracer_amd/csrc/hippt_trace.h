@@ -562,7 +562,11 @@ __device__ __forceinline__ unsigned child_key(float nx, float fx, float ny, floa
 
 // Byte offset of the near-plane row within a (lo, hi) row pair: 16 when the axis's reciprocal
 // direction is negative (its hi plane is entered first), else 0.
-__device__ __forceinline__ int near_row(float inv) { return int((__float_as_uint(inv) >> 27) & 16u); }
+__device__ __forceinline__ unsigned near_row(float inv) { return (__float_as_uint(inv) >> 27) & 16u; }
+
+__device__ __forceinline__ float4 ld4(const float4 *base, unsigned byteOffset) {
+    return *reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(base) + byteOffset);
+}
 
 // Compare-exchange of (key, child code) pairs: afterwards ka <= kb.
 __device__ __forceinline__ void cas(unsigned &ka, int &ca, unsigned &kb, int &cb) {
@@ -583,19 +587,19 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
                                                     unsigned long long &ntest, unsigned *pc, unsigned leafExit,
                                                     unsigned nodeExit, const SpillArea &S) {
     const float tmin = 0.001f;
-    const int sx = near_row(r.ix), sy = near_row(r.iy), sz = near_row(r.iz);
+    const unsigned sx = near_row(r.ix), sy = near_row(r.iy), sz = near_row(r.iz);
     while (T.cur >= 0) {
         prof<STATS>(pc, 3);
-        const float4 *nd = nodes + __umul24(unsigned(T.cur), unsigned(NODE_F4));
-        // rows lo.x hi.x lo.y hi.y lo.z hi.z: read as near/far rows of this ray's octant
-        const char *nb = reinterpret_cast<const char *>(nd);
-        const float4 nx = *reinterpret_cast<const float4 *>(nb + sx);
-        const float4 fx = *reinterpret_cast<const float4 *>(nb - sx + 16);
-        const float4 ny = *reinterpret_cast<const float4 *>(nb + sy + 32);
-        const float4 fy = *reinterpret_cast<const float4 *>(nb - sy + 48);
-        const float4 nz = *reinterpret_cast<const float4 *>(nb + sz + 64);
-        const float4 fz = *reinterpret_cast<const float4 *>(nb - sz + 80);
-        const int4 ch = *reinterpret_cast<const int4 *>(nd + 6);
+        // rows lo.x hi.x lo.y hi.y lo.z hi.z: read as near/far rows of this ray's octant (32-bit
+        // byte offsets from the uniform base: base-register + offset-register loads)
+        const unsigned nb = __umul24(unsigned(T.cur), unsigned(NODE_F4 * 16));
+        const float4 nx = ld4(nodes, nb + sx);
+        const float4 fx = ld4(nodes, nb + (sx ^ 16u));
+        const float4 ny = ld4(nodes, nb + sy + 32u);
+        const float4 fy = ld4(nodes, nb + (sy ^ 16u) + 32u);
+        const float4 nz = ld4(nodes, nb + sz + 64u);
+        const float4 fz = ld4(nodes, nb + (sz ^ 16u) + 64u);
+        const int4 ch = *reinterpret_cast<const int4 *>(reinterpret_cast<const char *>(nodes) + nb + 96u);
         if (STATS) ++nvis;
         unsigned k0 = child_key(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, r, tmin, T.bestT);
         unsigned k1 = child_key(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, r, tmin, T.bestT);

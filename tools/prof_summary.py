@@ -60,7 +60,7 @@ def main():
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed]
     mean_ms = statistics.mean(durs)
     c = {}
-    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2"):
+    for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2", "pmc_ta"):
         p = os.path.join(root, sub, "run_counter_collection.csv")
         if os.path.exists(p):
             vals, n = counters(p, lps)
@@ -91,6 +91,12 @@ def main():
         "wait_inst_any_frac": round(c["SQ_WAIT_INST_ANY"] / c["SQ_WAVE_CYCLES"], 4) if c.get("SQ_WAVE_CYCLES") else None,
         "active_inst_any_frac": round(c["SQ_ACTIVE_INST_ANY"] / c["SQ_WAVE_CYCLES"], 4)
         if c.get("SQ_WAVE_CYCLES") and c.get("SQ_ACTIVE_INST_ANY") else None,
+        # texture-addresser (vector-memory address unit) busy fraction per CU: the limiter of
+        # global-memory BVH traversal (every lane's node/triangle load passes through it)
+        "ta_busy": round(c["TA_BUSY_avr"] / (c["GRBM_GUI_ACTIVE"] / 8), 4)
+        if c.get("TA_BUSY_avr") and c.get("GRBM_GUI_ACTIVE") else None,
+        "ta_cycles_per_vmem_wave": round(c["TA_BUSY_avr"] * cus / c["TA_FLAT_READ_WAVEFRONTS_sum"], 2)
+        if c.get("TA_BUSY_avr") and c.get("TA_FLAT_READ_WAVEFRONTS_sum") else None,
         "bench_value_msamples_s": bench["value"],
     }
     prof_dir = os.path.join(repo, "profiles")

@@ -24,4 +24,6 @@ timeout -k 10 300 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_
     python3 bench.py "${ARGS[@]}" > "$OUT/pmc_sq.json" 2> "$OUT/pmc_sq.err"
 timeout -k 10 300 rocprofv3 --pmc SQ_ACTIVE_INST_VALU SQ_INST_CYCLES_VMEM_RD SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_ANY GRBM_GUI_ACTIVE -T --output-format csv -d "$OUT/pmc_sq2" -o run -- \
     python3 bench.py "${ARGS[@]}" > "$OUT/pmc_sq2.json" 2> "$OUT/pmc_sq2.err" || echo "pmc_sq2 pass failed (counter set)" >&2
+timeout -k 10 300 rocprofv3 --pmc TA_BUSY_avr TA_FLAT_READ_WAVEFRONTS_sum TD_TD_BUSY_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum GRBM_GUI_ACTIVE -T --output-format csv -d "$OUT/pmc_ta" -o run -- \
+    python3 bench.py "${ARGS[@]}" > "$OUT/pmc_ta.json" 2> "$OUT/pmc_ta.err" || echo "pmc_ta pass failed (counter set)" >&2
 echo "profile $TAG done"
