@@ -116,8 +116,8 @@ struct State {
     // options
     bool countTraversal = false;
     int waveThreshold = 32;
-    // one batch (and one end-of-batch tail) per 1080p/64-spp call: 132.7M samples x 12 B
-    long long scratchMB = 4096;
+    // one batch (and one end-of-batch tail) per call up to 4K/256 spp: 2.12G samples x 12 B
+    long long scratchMB = 32768;
     unsigned chunk = 256;
     int leafExit = -1;  // -1: automatic from the tree depth and LDS residency
     int nodeExit = -1;  // -1: automatic

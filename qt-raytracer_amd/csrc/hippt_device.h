@@ -35,7 +35,7 @@ struct MeshParams {
     // kShadeSphere); material index as int bits
     const float4 *shade;
     const float4 *mats;    // 2 float4 per material: (albedo rgb, kind) (fuzz, ir, -, -)
-    float *scratch;        // 3 planes (R, G, B) of totalItems floats: per-sample radiance
+    float *scratch;        // per-sample radiance, RGB float triples (12 B) in item order
     unsigned *queue;       // kQueues work counters, 128 B apart (zeroed before launch)
     unsigned long long *stats;  // [0] segments, [1] pixel samples, [2] node visits, [3] tri tests
     CameraF cam;

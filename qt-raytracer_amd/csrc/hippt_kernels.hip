@@ -294,9 +294,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? 7 : HIPPT_MESH_WAVES_P
                 finished = true;  // absorbed: contributes 0 (RayTracer.h:590)
             }
             if (finished) {
-                P.scratch[item] = Lr;
-                P.scratch[size_t(P.totalItems) + item] = Lg;
-                P.scratch[2 * size_t(P.totalItems) + item] = Lb;
+                store_radiance(P.scratch, item, Lr, Lg, Lb);
                 ++samples;
                 item = kNone;
                 need = true;
@@ -343,9 +341,10 @@ __global__ __launch_bounds__(256) void combine_kernel(CombineParams P) {
             const size_t k = size_t(fl) * P.bandPixels + p;
             const int f = P.firstFrame + fl;
             const float ff = float(f), fc = float(f + 1);
-            acc.x = fmaf(acc.x, ff, P.scratch[k]) / fc;
-            acc.y = fmaf(acc.y, ff, P.scratch[size_t(P.totalItems) + k]) / fc;
-            acc.z = fmaf(acc.z, ff, P.scratch[2 * size_t(P.totalItems) + k]) / fc;
+            const float3 L = *reinterpret_cast<const float3 *>(P.scratch + 3 * k);
+            acc.x = fmaf(acc.x, ff, L.x) / fc;
+            acc.y = fmaf(acc.y, ff, L.y) / fc;
+            acc.z = fmaf(acc.z, ff, L.z) / fc;
         }
         acc.w = 1.0f;
         P.accum[p] = acc;

@@ -239,6 +239,13 @@ __device__ __forceinline__ void camera_sample(const MeshParams &P, unsigned it, 
     r.dz = (fmaf(t, C.vertical[2], fmaf(s, C.horizontal[2], C.llc[2])) - C.origin[2]) - fz;
 }
 
+// A finished sample's radiance: one 12-byte store (one vector-memory instruction; three planes
+// cost three, and the store instructions of lanes finishing at different times dominated the
+// address unit's load on LDS-resident scenes).
+__device__ __forceinline__ void store_radiance(float *scratch, unsigned item, float r, float g, float b) {
+    *reinterpret_cast<float3 *>(scratch + 3 * size_t(item)) = make_float3(r, g, b);
+}
+
 // Sky gradient on a miss (RayTracer.h:593-595), times throughput.
 __device__ __forceinline__ void sky(const Ray &r, float tr, float tg, float tb, float &L0, float &L1, float &L2) {
     const float uy = (1.0f / sqrtf(fdot(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz))) * r.dy;

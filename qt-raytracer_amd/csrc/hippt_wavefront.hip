@@ -224,9 +224,7 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(WfParams W, int cur) {
             finished = true;  // absorbed: contributes 0
         }
         if (finished) {
-            P.scratch[q.item] = L0;
-            P.scratch[size_t(P.totalItems) + q.item] = L1;
-            P.scratch[2 * size_t(P.totalItems) + q.item] = L2;
+            store_radiance(P.scratch, q.item, L0, L1, L2);
         }
     }
     block_append(again, slot, cur ? W.extQ0 : W.extQ1, W.shardCap, W.ctr, kCtrExt0 + (cur ^ 1) * kWfShards, lds);
