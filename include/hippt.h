@@ -201,6 +201,9 @@ enum {
     , HIPPT_OPT_STACK_CAP = 18      /* 4-wide traversal: LDS stack entries per lane, 4..30 (deeper stacks spill
                                        to global memory); 0 (default): the tree's bound, at most 19 (30 for
                                        LDS scenes) */
+    , HIPPT_OPT_BVH_QUANT = 19      /* 4-wide traversal of global-memory trees over 64-byte nodes with 8-bit
+                                       child boxes (1) or 128-byte float nodes (0); -1 (default): 8-bit for
+                                       Lambertian-triangle scenes */
 };
 bool hipptSetOption(int key, long long value);
 long long hipptGetOption(int key);
@@ -228,6 +231,11 @@ int hipptBvh4NodeCount(const hipptBvh *bvh);
 int hipptBvh4Depth(const hipptBvh *bvh);
 int hipptBvh4StackBound(const hipptBvh *bvh);
 void hipptBvh4Copy(const hipptBvh *bvh, uint32_t *nodes);
+/* The same 4-wide tree with 8-bit child boxes (HIPPT_OPT_BVH_QUANT), Bvh4NodeCount nodes of 16
+ * words: origin xyz (float), scale x; lo.x hi.x lo.y hi.y lo.z hi.z (4 bytes each, byte i =
+ * child i, plane = origin + byte * scale); scale y; scale z; child[4].  Every decoded box
+ * contains the float box of hipptBvh4Copy; an unused slot has lo bytes 255 and hi bytes 0. */
+void hipptBvh4QCopy(const hipptBvh *bvh, uint32_t *nodes);
 
 #ifdef __cplusplus
 }

@@ -389,4 +389,61 @@ void collapse_bvh4(const Bvh &bvh2, Bvh4 &out) {
     Collapser(bvh2, out).emit(0, 0, 1);
 }
 
+void quantize_bvh4(const Bvh4 &in, std::vector<uint32_t> &out) {
+    const size_t n = in.nodes.size() / kNode4Words;
+    out.assign(n * kNode4QWords, 0u);
+    const int32_t unused = leaf_code(0, 0);
+    for (size_t k = 0; k < n; ++k) {
+        const uint32_t *w = &in.nodes[k * kNode4Words];
+        float f[24];
+        std::memcpy(f, w, sizeof(f));
+        uint32_t *d = &out[k * kNode4QWords];
+        bool used[4];
+        for (int i = 0; i < 4; ++i) used[i] = int32_t(w[24 + i]) != unused;
+        uint32_t qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
+        float origin[3], scale[3];
+        for (int a = 0; a < 3; ++a) {
+            float lo = INFINITY, hi = -INFINITY;
+            for (int i = 0; i < 4; ++i)
+                if (used[i]) {
+                    lo = std::min(lo, f[8 * a + i]);
+                    hi = std::max(hi, f[8 * a + 4 + i]);
+                }
+            if (!(lo <= hi)) lo = hi = 0.0f;  // no used child (never built; kept total)
+            // smallest power-of-two scale with 255 steps covering [lo, hi] (the differences are
+            // exact in double, the scale and the floor/ceil too)
+            const double ext = double(hi) - double(lo);
+            int e = -100;
+            if (ext > 0) {
+                e = int(std::ceil(std::log2(ext / 255.0)));
+                while (std::ldexp(255.0, e) < ext) ++e;
+                while (e > -100 && std::ldexp(255.0, e - 1) >= ext) --e;
+                e = std::max(e, -100);
+            }
+            origin[a] = lo;
+            scale[a] = float(std::ldexp(1.0, e));
+            for (int i = 0; i < 4; ++i) {
+                uint32_t ql = 255, qh = 0;  // unused: lo > hi on every axis
+                if (used[i]) {
+                    const double l = std::floor((double(f[8 * a + i]) - double(lo)) / scale[a]);
+                    const double h = std::ceil((double(f[8 * a + 4 + i]) - double(lo)) / scale[a]);
+                    ql = uint32_t(std::clamp(l, 0.0, 255.0));
+                    qh = uint32_t(std::clamp(h, 0.0, 255.0));
+                }
+                qlo[a] |= ql << (8 * i);
+                qhi[a] |= qh << (8 * i);
+            }
+        }
+        std::memcpy(&d[0], origin, 3 * sizeof(float));
+        std::memcpy(&d[3], &scale[0], sizeof(float));
+        for (int a = 0; a < 3; ++a) {
+            d[4 + 2 * a] = qlo[a];
+            d[5 + 2 * a] = qhi[a];
+        }
+        std::memcpy(&d[10], &scale[1], sizeof(float));
+        std::memcpy(&d[11], &scale[2], sizeof(float));
+        for (int i = 0; i < 4; ++i) d[12 + i] = w[24 + i];
+    }
+}
+
 }  // namespace hippt

@@ -61,4 +61,16 @@ struct Bvh4 {
 };
 void collapse_bvh4(const Bvh &bvh2, Bvh4 &out);
 
+// The 4-wide tree with 8-bit child boxes (Ylitie et al. 2017, "Efficient incoherent ray traversal
+// on GPUs through compressed wide BVHs", reduced to 4 children): 64-byte nodes, same node
+// indices, child codes and primitive order as Bvh4.  Words:
+//   0-2  grid origin o (float xyz)           3   scale s.x (a power of two)
+//   4-9  lo.x hi.x lo.y hi.y lo.z hi.z: byte i = child i's plane q, plane = o + q*s
+//   10   scale s.y   11  scale s.z           12-15 child codes
+// Planes are rounded outward (lo down, hi up), so every decoded box contains the Bvh4 box (which
+// is already padded for the kernel's slab-test rounding).  An unused child slot has lo = 255,
+// hi = 0 on every axis: read as near/far planes by the ray's octant it is always missed.
+constexpr int kNode4QWords = 16;
+void quantize_bvh4(const Bvh4 &in, std::vector<uint32_t> &out);
+
 }  // namespace hippt

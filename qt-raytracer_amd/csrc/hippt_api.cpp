@@ -29,6 +29,7 @@
 struct hipptBvh {
     hippt::Bvh bvh;
     hippt::Bvh4 bvh4;
+    std::vector<uint32_t> bvh4q;
 };
 
 namespace {
@@ -59,6 +60,7 @@ struct Ctx {
     int sceneVersion = -1;
     float4 *nodes = nullptr, *tris = nullptr, *shade = nullptr, *mats = nullptr;
     float4 *nodes4 = nullptr;  // 4-wide BVH (same primitive order as nodes)
+    float4 *nodes4q = nullptr; // the 4-wide BVH with 8-bit child boxes
     int *spill = nullptr;      // 4-wide traversal: per-lane stack spill area
     size_t spillBytes = 0;
     // wavefront path-state pool (allocated on first use)
@@ -84,6 +86,7 @@ struct SceneHost {
     std::vector<float4> nodes, tris, shade, mats;  // device layouts (hippt_device.h MeshParams)
     int numTris = 0, numNodes = 0, levels = 0;  // numTris: primitive records (triangles + spheres)
     std::vector<float4> nodes4;                 // 4-wide BVH (bvh_builder.h Bvh4)
+    std::vector<float4> nodes4q;                // quantize_bvh4 of it
     int numNodes4 = 0, levels4 = 0, stackBound4 = 0;
     bool full = false;                          // spheres or non-Lambertian materials
     double lookfrom[3] = {0, 0, 0}, lookat[3] = {0, 0, -1}, vup[3] = {0, 1, 0};
@@ -123,6 +126,7 @@ struct State {
     int nodeExit = -1;  // -1: automatic
     int bvhWidth = 0;   // megakernel traversal over the 2- or 4-wide BVH; 0: 4-wide if it fits in LDS
     int stackCap = 0;   // 4-wide LDS stack entries (0: automatic)
+    int bvhQuant = -1;  // 4-wide global-memory traversal over 8-bit child boxes (-1: automatic)
     int activeWidth = 0;  // BVH width of the last mesh render (hipptActiveBvhWidth)
     int blocksPerCu = 0;
     bool ldsScene = true;
@@ -212,7 +216,8 @@ void free_scene_buffers(Ctx &c) {
     (void)hipFree(c.shade);
     (void)hipFree(c.mats);
     (void)hipFree(c.nodes4);
-    c.nodes = c.tris = c.shade = c.mats = c.nodes4 = nullptr;
+    (void)hipFree(c.nodes4q);
+    c.nodes = c.tris = c.shade = c.mats = c.nodes4 = c.nodes4q = nullptr;
     c.sceneVersion = -1;
 }
 
@@ -311,7 +316,7 @@ bool ensure_scene(Ctx &c, const char **err) {
         return true;
     };
     if (!up(c.nodes, s.scene.nodes) || !up(c.tris, s.scene.tris) || !up(c.shade, s.scene.shade) ||
-        !up(c.mats, s.scene.mats) || !up(c.nodes4, s.scene.nodes4))
+        !up(c.mats, s.scene.mats) || !up(c.nodes4, s.scene.nodes4) || !up(c.nodes4q, s.scene.nodes4q))
         return false;
     c.sceneVersion = s.scene.version;
     return true;
@@ -382,8 +387,9 @@ bool init_locked(int width, int height, const char **err) {
     return false;
 }
 
-long long occupancy_key(int version, int stackDepth, bool lds, bool full, bool wide = false) {
-    return ((long long)version << 9) | (stackDepth << 3) | (wide ? 4 : 0) | (lds ? 2 : 0) | (full ? 1 : 0);
+long long occupancy_key(int version, int stackDepth, bool lds, bool full, bool wide = false, bool quant = false) {
+    return ((long long)version << 10) | (stackDepth << 4) | (quant ? 8 : 0) | (wide ? 4 : 0) | (lds ? 2 : 0) |
+           (full ? 1 : 0);
 }
 
 // Wavefront variant (hippt_wavefront.hip): init + generate, then extend/shade/generate
@@ -538,11 +544,19 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 const int stackCap = wide ? std::max(1, std::min(s.scene.stackBound4, capLimit)) : 0;
                 const int stackDepth = wide ? stackCap + 2 : std::max(1, s.scene.levels);
                 const bool spills = wide && s.scene.stackBound4 > stackCap;
-                const long long occKey = occupancy_key(s.scene.version, stackDepth, ldsScene, s.scene.full, wide);
+                // 8-bit child boxes for trees read from global memory: 64-byte nodes, 4 vector loads
+                // instead of 7 where the texture addresser bounds the traversal (blob70k: TA busy
+                // 84%, 15.6 -> 17.7 G).  Automatic for the Lambertian-triangle kernel only
+                // (random_scene, general kernel: 20.9 -> 18.5 G).
+                const bool quant = wide && !ldsScene && (s.bvhQuant == 1 || (s.bvhQuant == -1 && !s.scene.full));
+                const long long occKey =
+                    occupancy_key(s.scene.version, stackDepth, ldsScene, s.scene.full, wide, quant);
                 if (c.occKey != occKey) {
                     const int ln = ldsScene ? numNodes : 0, lt = ldsScene ? numTris : 0;
-                    c.meshBlocksPerCu[0] = hippt::mesh_blocks_per_cu(false, s.scene.full, wide, stackDepth, ln, lt);
-                    c.meshBlocksPerCu[1] = hippt::mesh_blocks_per_cu(true, s.scene.full, wide, stackDepth, ln, lt);
+                    c.meshBlocksPerCu[0] =
+                        hippt::mesh_blocks_per_cu(false, s.scene.full, wide, quant, stackDepth, ln, lt);
+                    c.meshBlocksPerCu[1] =
+                        hippt::mesh_blocks_per_cu(true, s.scene.full, wide, quant, stackDepth, ln, lt);
                     c.occKey = occKey;
                 }
                 int bpc = s.blocksPerCu > 0 ? s.blocksPerCu : c.meshBlocksPerCu[cnt ? 1 : 0];
@@ -554,7 +568,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         HIP_TRY(hipMemsetAsync(c.scratch, 0, size_t(total) * 3 * sizeof(float), c.stream));
                     } else {
                         hippt::MeshParams p{};
-                        p.nodes = wide ? c.nodes4 : c.nodes;
+                        p.nodes = quant ? c.nodes4q : wide ? c.nodes4 : c.nodes;
                         p.tris = c.tris;
                         p.shade = c.shade;
                         p.mats = c.mats;
@@ -590,7 +604,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.leafExit = unsigned(s.leafExit >= 0 ? s.leafExit
                                                               : ldsScene ? 4 : std::clamp(s.scene.levels - 6, 0, 16));
                         p.nodeExit = unsigned(s.nodeExit >= 0 ? s.nodeExit : 48);
-                        p.wide = wide ? 1 : 0;
+                        p.wide = quant ? 2 : wide ? 1 : 0;
                         p.stackCap = stackCap;
                         if (s.pathMode == 1) {
                             if (!run_wavefront(c, p, cnt, err)) return false;
@@ -763,6 +777,10 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
     sc.nodes4.assign(bvh4.nodes.size() / 4, float4{});
     std::memcpy(sc.nodes4.data(), bvh4.nodes.data(), bvh4.nodes.size() * sizeof(uint32_t));
     sc.numNodes4 = int(bvh4.nodes.size() / hippt::kNode4Words);
+    std::vector<uint32_t> q;
+    hippt::quantize_bvh4(bvh4, q);
+    sc.nodes4q.assign(q.size() / 4, float4{});
+    std::memcpy(sc.nodes4q.data(), q.data(), q.size() * sizeof(uint32_t));
     sc.levels4 = bvh4.levels;
     sc.stackBound4 = bvh4.stackBound;
     sc.tris.assign(size_t(numPrims) * 3, float4{});
@@ -1135,6 +1153,10 @@ extern "C" bool hipptSetOption(int key, long long value) {
         if (value != 0 && (value < 4 || value > 30)) return false;
         s.stackCap = int(value);
         return true;
+    case HIPPT_OPT_BVH_QUANT:
+        if (value < -1 || value > 1) return false;
+        s.bvhQuant = int(value);
+        return true;
     default: return false;
     }
 }
@@ -1165,6 +1187,7 @@ extern "C" long long hipptGetOption(int key) {
     case HIPPT_OPT_BVH_SAH: return s.bvh.sahMode;
     case HIPPT_OPT_BVH_WIDTH: return s.bvhWidth;
     case HIPPT_OPT_STACK_CAP: return s.stackCap;
+    case HIPPT_OPT_BVH_QUANT: return s.bvhQuant;
     default: return -1;
     }
 }
@@ -1187,6 +1210,7 @@ extern "C" hipptBvh *hipptBvhBuild(const float *verts, int numTris, float extent
         return nullptr;
     }
     hippt::collapse_bvh4(b->bvh, b->bvh4);
+    hippt::quantize_bvh4(b->bvh4, b->bvh4q);
     return b;
 }
 
@@ -1205,4 +1229,7 @@ extern "C" int hipptBvh4Depth(const hipptBvh *b) { return b ? b->bvh4.levels : 0
 extern "C" int hipptBvh4StackBound(const hipptBvh *b) { return b ? b->bvh4.stackBound : 0; }
 extern "C" void hipptBvh4Copy(const hipptBvh *b, uint32_t *nodes) {
     if (b && nodes) std::memcpy(nodes, b->bvh4.nodes.data(), b->bvh4.nodes.size() * sizeof(uint32_t));
+}
+extern "C" void hipptBvh4QCopy(const hipptBvh *b, uint32_t *nodes) {
+    if (b && nodes) std::memcpy(nodes, b->bvh4q.data(), b->bvh4q.size() * sizeof(uint32_t));
 }

@@ -52,8 +52,9 @@ struct MeshParams {
     unsigned chunk;        // items per queue grab (multiple of 64)
     unsigned leafExit;     // node loop exits once <= leafExit lanes still search for a leaf
     unsigned nodeExit;     // leaf loop exits once <= nodeExit lanes still hold a leaf (0: never)
-    // 4-wide BVH (nodes = Bvh4 layout, 8 float4 per node): LDS stack content capacity and the
-    // per-lane spill area (spillCap entries per lane of the persistent grid; null if never used)
+    // 4-wide BVH: wide = 1 (Bvh4 layout, 8 float4 per node) or 2 (quantize_bvh4 layout, 4 float4
+    // per node; global-memory scenes only); LDS stack content capacity and the per-lane spill
+    // area (spillCap entries per lane of the persistent grid; null if never used)
     int wide;
     int stackCap;
     int spillCap;
@@ -78,7 +79,8 @@ hipError_t launch_sphere4(const Sphere4Params &p, hipStream_t s);
 hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hipStream_t s);
 hipError_t launch_combine(const CombineParams &p, hipStream_t s);
 // Resident mesh-kernel blocks per CU for a given LDS stack depth and LDS scene size.
-int mesh_blocks_per_cu(bool countTraversal, bool full, bool wide, int stackDepth, int ldsNodes, int ldsTris);
+int mesh_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,
+                       int ldsTris);
 size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide);
 size_t mesh_lds_scene_limit();
 constexpr int kMeshBlock = 256;

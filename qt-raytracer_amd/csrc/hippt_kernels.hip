@@ -184,8 +184,9 @@ __device__ unsigned long long g_timeline[65536 * 6];
 #endif
 #define HIPPT_SGPR_ATTR __attribute__((amdgpu_num_sgpr(HIPPT_NUM_SGPR)))
 
-template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE>
+template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE, bool QUANT>
 __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? 7 : HIPPT_MESH_WAVES_PER_EU) HIPPT_SGPR_ATTR void mesh_kernel(MeshParams P) {
+    static_assert(!QUANT || (WIDE && !LDS_SCENE), "quantized nodes: 4-wide global-memory traversal only");
 #ifdef HIPPT_DEBUG_TIMELINE
     const unsigned tlw = blockIdx.x * 4u + (threadIdx.x >> 6);
     unsigned long long tlDrained = 0, tlItems = 0;
@@ -221,7 +222,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? 7 : HIPPT_MESH_WAVES_P
         tris = sTris;
         shade = sShade;
     }
-    constexpr int nodeF4 = LDS_SCENE ? ldsNodeF4 : (WIDE ? 8 : 4);
+    constexpr int nodeF4 = LDS_SCENE ? ldsNodeF4 : (WIDE ? (QUANT ? 4 : 8) : 4);
     const SpillArea S{P.spill, (blockIdx.x * unsigned(kMeshBlock) + threadIdx.x) * unsigned(P.spillCap), P.stackCap};
 
     WorkQueue Q;
@@ -270,8 +271,8 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? 7 : HIPPT_MESH_WAVES_P
         do {
             prof<STATS>(pc, 2);
             if (WIDE)
-                traverse_round_wide<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit,
-                                                         P.nodeExit, S);
+                traverse_round_wide<nodeF4, STATS, FULL, QUANT>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit,
+                                                                P.nodeExit, S);
             else
                 traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
         } while (__popcll(__ballot(busy(T))) > unsigned(P.waveThreshold));
@@ -385,17 +386,16 @@ size_t mesh_lds_scene_limit() { return 24u << 10; }
 static constexpr int kMaxResidentBlocks = 800 / (HIPPT_NUM_SGPR + 16) < 8 ? 800 / (HIPPT_NUM_SGPR + 16) : 8;
 
 using MeshFn = void (*)(MeshParams);
-template <bool STATS, bool FULL, bool WIDE>
-static MeshFn mesh_fn_lds(bool lds) {
-    return lds ? mesh_kernel<STATS, true, FULL, WIDE> : mesh_kernel<STATS, false, FULL, WIDE>;
-}
+// node formats: 2-wide, 4-wide float, 4-wide quantized (global memory only)
 template <bool STATS, bool FULL>
-static MeshFn mesh_fn_wide(bool lds, bool wide) {
-    return wide ? mesh_fn_lds<STATS, FULL, true>(lds) : mesh_fn_lds<STATS, FULL, false>(lds);
+static MeshFn mesh_fn_fmt(bool lds, bool wide, bool quant) {
+    if (lds) return wide ? mesh_kernel<STATS, true, FULL, true, false> : mesh_kernel<STATS, true, FULL, false, false>;
+    if (!wide) return mesh_kernel<STATS, false, FULL, false, false>;
+    return quant ? mesh_kernel<STATS, false, FULL, true, true> : mesh_kernel<STATS, false, FULL, true, false>;
 }
-static MeshFn mesh_fn(bool count, bool lds, bool full, bool wide) {
-    if (count) return full ? mesh_fn_wide<true, true>(lds, wide) : mesh_fn_wide<true, false>(lds, wide);
-    return full ? mesh_fn_wide<false, true>(lds, wide) : mesh_fn_wide<false, false>(lds, wide);
+static MeshFn mesh_fn(bool count, bool lds, bool full, bool wide, bool quant) {
+    if (count) return full ? mesh_fn_fmt<true, true>(lds, wide, quant) : mesh_fn_fmt<true, false>(lds, wide, quant);
+    return full ? mesh_fn_fmt<false, true>(lds, wide, quant) : mesh_fn_fmt<false, false>(lds, wide, quant);
 }
 
 hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hipStream_t s) {
@@ -403,8 +403,8 @@ hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hip
     if (p.wide && (p.stackCap < 1 || p.stackCap + 2 > p.stackDepth)) return hipErrorInvalidValue;
     const bool lds = p.ldsScene != 0;
     const size_t bytes = mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0, p.wide != 0);
-    hipLaunchKernelGGL(mesh_fn(countTraversal, lds, p.full != 0, p.wide != 0), dim3(blocks), dim3(kMeshBlock), bytes,
-                       s, p);
+    hipLaunchKernelGGL(mesh_fn(countTraversal, lds, p.full != 0, p.wide != 0, p.wide == 2 && !lds), dim3(blocks),
+                       dim3(kMeshBlock), bytes, s, p);
     return hipGetLastError();
 }
 
@@ -416,12 +416,13 @@ hipError_t launch_combine(const CombineParams &p, hipStream_t s) {
     return hipGetLastError();
 }
 
-int mesh_blocks_per_cu(bool countTraversal, bool full, bool wide, int stackDepth, int ldsNodes, int ldsTris) {
+int mesh_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,
+                       int ldsTris) {
     int n = 0;
     const bool lds = ldsNodes > 0;
     const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, wide);
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, mesh_fn(countTraversal, lds, full, wide),
-                                                                kMeshBlock, bytes);
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &n, mesh_fn(countTraversal, lds, full, wide, quant && wide && !lds), kMeshBlock, bytes);
     if (e != hipSuccess || n <= 0) n = 1;
     // the query ignores the trap handler's SGPRs (kMaxResidentBlocks): a larger persistent grid
     // leaves blocks waiting for a slot until others finish

@@ -567,6 +567,20 @@ __device__ __forceinline__ unsigned child_key(float nx, float fx, float ny, floa
     return n <= f ? __float_as_uint(n) : 0xffffffffu;
 }
 
+// child_key over a quantized node: byte I of each plane word (v_cvt_f32_ubyteI), scaled
+// and offset per axis (t = q*B + A).
+template <int I>
+__device__ __forceinline__ unsigned child_key_q(unsigned nxw, unsigned fxw, unsigned nyw, unsigned fyw, unsigned nzw,
+                                                unsigned fzw, float ax, float bx, float ay, float by, float az,
+                                                float bz, float tmin, float bestT) {
+    const float tnx = fmaf(float((nxw >> (8 * I)) & 0xffu), bx, ax), tfx = fmaf(float((fxw >> (8 * I)) & 0xffu), bx, ax);
+    const float tny = fmaf(float((nyw >> (8 * I)) & 0xffu), by, ay), tfy = fmaf(float((fyw >> (8 * I)) & 0xffu), by, ay);
+    const float tnz = fmaf(float((nzw >> (8 * I)) & 0xffu), bz, az), tfz = fmaf(float((fzw >> (8 * I)) & 0xffu), bz, az);
+    const float n = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
+    const float f = fminf(fminf(tfx, tfy), fminf(tfz, bestT));
+    return n <= f ? __float_as_uint(n) : 0xffffffffu;
+}
+
 // Byte offset of the near-plane row within a (lo, hi) row pair: 16 when the axis's reciprocal
 // direction is negative (its hi plane is entered first), else 0.
 __device__ __forceinline__ unsigned near_row(float inv) { return (__float_as_uint(inv) >> 27) & 16u; }
@@ -588,7 +602,7 @@ __device__ __forceinline__ void cas(unsigned &ka, int &ca, unsigned &kb, int &cb
 
 // traverse_round over the 4-wide tree: a node visit tests its four child boxes, descends into
 // the nearest hit child and pushes the other hit children far to near.
-template <int NODE_F4, bool STATS, bool FULL>
+template <int NODE_F4, bool STATS, bool FULL, bool QUANT = false>
 __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *my, const float4 *nodes,
                                                     const float4 *tris, unsigned long long &nvis,
                                                     unsigned long long &ntest, unsigned *pc, unsigned leafExit,
@@ -600,18 +614,40 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
         // rows lo.x hi.x lo.y hi.y lo.z hi.z: read as near/far rows of this ray's octant (32-bit
         // byte offsets from the uniform base: base-register + offset-register loads)
         const unsigned nb = __umul24(unsigned(T.cur), unsigned(NODE_F4 * 16));
-        const float4 nx = ld4(nodes, nb + sx);
-        const float4 fx = ld4(nodes, nb + (sx ^ 16u));
-        const float4 ny = ld4(nodes, nb + sy + 32u);
-        const float4 fy = ld4(nodes, nb + (sy ^ 16u) + 32u);
-        const float4 nz = ld4(nodes, nb + sz + 64u);
-        const float4 fz = ld4(nodes, nb + (sz ^ 16u) + 64u);
-        const int4 ch = *reinterpret_cast<const int4 *>(reinterpret_cast<const char *>(nodes) + nb + 96u);
+        unsigned k0, k1, k2, k3;
+        int4 ch;
+        if (!QUANT) {
+            const float4 nx = ld4(nodes, nb + sx);
+            const float4 fx = ld4(nodes, nb + (sx ^ 16u));
+            const float4 ny = ld4(nodes, nb + sy + 32u);
+            const float4 fy = ld4(nodes, nb + (sy ^ 16u) + 32u);
+            const float4 nz = ld4(nodes, nb + sz + 64u);
+            const float4 fz = ld4(nodes, nb + (sz ^ 16u) + 64u);
+            ch = *reinterpret_cast<const int4 *>(reinterpret_cast<const char *>(nodes) + nb + 96u);
+            k0 = child_key(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, r, tmin, T.bestT);
+            k1 = child_key(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, r, tmin, T.bestT);
+            k2 = child_key(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z, r, tmin, T.bestT);
+            k3 = child_key(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w, r, tmin, T.bestT);
+        } else {
+            // 64-byte node (bvh_builder.h quantize_bvh4): 4 loads instead of 7.  Plane q of axis
+            // a enters the slab test as t = q*(s*inv) + (o*inv - o_ray*inv).
+            const float4 o = ld4(nodes, nb);
+            const uint4 q = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(nodes) + nb + 16u);
+            const float4 q2 = ld4(nodes, nb + 32u);
+            ch = *reinterpret_cast<const int4 *>(reinterpret_cast<const char *>(nodes) + nb + 48u);
+            const float bx = o.w * r.ix, ax = fmaf(o.x, r.ix, -r.oix);
+            const float by = q2.z * r.iy, ay = fmaf(o.y, r.iy, -r.oiy);
+            const float bz = q2.w * r.iz, az = fmaf(o.z, r.iz, -r.oiz);
+            const unsigned qlz = __float_as_uint(q2.x), qhz = __float_as_uint(q2.y);
+            const unsigned nxw = sx ? q.y : q.x, fxw = sx ? q.x : q.y;
+            const unsigned nyw = sy ? q.w : q.z, fyw = sy ? q.z : q.w;
+            const unsigned nzw = sz ? qhz : qlz, fzw = sz ? qlz : qhz;
+            k0 = child_key_q<0>(nxw, fxw, nyw, fyw, nzw, fzw, ax, bx, ay, by, az, bz, tmin, T.bestT);
+            k1 = child_key_q<1>(nxw, fxw, nyw, fyw, nzw, fzw, ax, bx, ay, by, az, bz, tmin, T.bestT);
+            k2 = child_key_q<2>(nxw, fxw, nyw, fyw, nzw, fzw, ax, bx, ay, by, az, bz, tmin, T.bestT);
+            k3 = child_key_q<3>(nxw, fxw, nyw, fyw, nzw, fzw, ax, bx, ay, by, az, bz, tmin, T.bestT);
+        }
         if (STATS) ++nvis;
-        unsigned k0 = child_key(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, r, tmin, T.bestT);
-        unsigned k1 = child_key(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, r, tmin, T.bestT);
-        unsigned k2 = child_key(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z, r, tmin, T.bestT);
-        unsigned k3 = child_key(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w, r, tmin, T.bestT);
         const int nh = int(k0 != 0xffffffffu) + int(k1 != 0xffffffffu) + int(k2 != 0xffffffffu) +
                        int(k3 != 0xffffffffu);
         // sorting network (0,1)(2,3)(0,2)(1,3)(1,2), codes carried along: c0 nearest

@@ -43,6 +43,7 @@ OPT_NODE_EXIT = 15
 OPT_BVH_SAH = 16
 OPT_BVH_WIDTH = 17
 OPT_STACK_CAP = 18
+OPT_BVH_QUANT = 19
 
 # Every symbol include/hippt.h declares (checked by tests/test_abi_cpu.py).
 EXPORTS = (
@@ -56,7 +57,8 @@ EXPORTS = (
     "hipptResetAccumulation", "hipptGetStats", "hipptResetStats", "hipptGetCounters", "hipptSetOption",
     "hipptGetOption",
     "hipptLastError", "hipptBvhBuild", "hipptBvhNodeCount", "hipptBvhDepth", "hipptBvhCopy", "hipptBvhFree",
-    "hipptBvh4NodeCount", "hipptBvh4Depth", "hipptBvh4StackBound", "hipptBvh4Copy", "hipptActiveBvhWidth",
+    "hipptBvh4NodeCount", "hipptBvh4Depth", "hipptBvh4StackBound", "hipptBvh4Copy", "hipptBvh4QCopy",
+    "hipptActiveBvhWidth",
 )
 
 
@@ -161,6 +163,7 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     sig("hipptBvh4Depth", c_int, ctypes.c_void_p)
     sig("hipptBvh4StackBound", c_int, ctypes.c_void_p)
     sig("hipptBvh4Copy", None, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32))
+    sig("hipptBvh4QCopy", None, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32))
     _lib = lib
     return lib
 
@@ -223,6 +226,8 @@ class Bvh:
             self.stack_bound4 = lib.hipptBvh4StackBound(h)
             self.nodes4 = np.zeros((lib.hipptBvh4NodeCount(h), 32), dtype=np.uint32)
             lib.hipptBvh4Copy(h, _ptr(self.nodes4, ctypes.c_uint32))
+            self.nodes4q = np.zeros((self.nodes4.shape[0], 16), dtype=np.uint32)
+            lib.hipptBvh4QCopy(h, _ptr(self.nodes4q, ctypes.c_uint32))
         finally:
             lib.hipptBvhFree(h)
 

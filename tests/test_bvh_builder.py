@@ -151,3 +151,38 @@ def test_bvh4_collapse_keeps_leaves_and_bounds_subtrees(name):
     assert seen.all()
     assert sorted(leaves4) == leaves2
     assert bound == bvh.stack_bound4 and depth == bvh.depth4
+
+
+@pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene", "cornell_mixed"])
+def test_bvh4_quantized_boxes_contain_float_boxes(name):
+    """quantize_bvh4 (hipptBvh4QCopy): every child box decoded exactly (origin + byte * scale, a
+    power-of-two scale) contains the float 4-wide box, each axis uses at most 255 steps of its
+    node's extent, codes are unchanged, and unused slots are inverted (lo 255 > hi 0) boxes."""
+    sc = scenes.get_scene(name)
+    if sc.num_tris == 0:
+        pytest.skip("sphere-only scene")
+    bvh = hippt.Bvh(sc.verts, extent_hint=800.0)
+    f, kids = _decode4(bvh.nodes4)
+    q = bvh.nodes4q
+    assert q.shape == (len(kids), 16)
+    origin = q[:, 0:3].view(np.float32).astype(np.float64)
+    scale = np.stack([q[:, 3], q[:, 10], q[:, 11]], axis=1).view(np.float32).astype(np.float64)
+    m, e = np.frexp(scale)
+    assert np.all(m == 0.5), "scales are powers of two"
+    planes = q[:, 4:10].view(np.uint8).reshape(-1, 3, 2, 4).astype(np.float64)  # node, axis, lo/hi, slot
+    assert np.array_equal(q[:, 12:16].view(np.int32), kids)
+    for n in range(len(kids)):
+        for c in range(4):
+            unused = kids[n, c] == -1 and f[n, 0, 0, c] > 1e37
+            if unused:
+                assert np.all(planes[n, :, 0, c] == 255) and np.all(planes[n, :, 1, c] == 0)
+                continue
+            lo = origin[n] + planes[n, :, 0, c] * scale[n]
+            hi = origin[n] + planes[n, :, 1, c] * scale[n]
+            assert np.all(lo <= f[n, :, 0, c].astype(np.float64))
+            assert np.all(hi >= f[n, :, 1, c].astype(np.float64))
+        # the scale is the smallest power of two whose 255 steps cover the node's extent
+        used = [c for c in range(4) if not (kids[n, c] == -1 and f[n, 0, 0, c] > 1e37)]
+        ext = f[n, :, 1, used].max(axis=0).astype(np.float64) - f[n, :, 0, used].min(axis=0).astype(np.float64)
+        assert np.all(255 * scale[n] >= ext)
+        assert np.all((ext == 0) | (255 * scale[n] / 2 < ext))

@@ -23,11 +23,11 @@ def pt():
     t.setRowRange(0, 0)
     t.setOption(hippt.OPT_DEVICE_ROWS, 1)
     t.useBuiltinScene(hippt.SCENE_SPHERE4)
-    for k, v in ((hippt.OPT_WAVE_THRESHOLD, 32), (hippt.OPT_SCRATCH_MB, 4096), (hippt.OPT_CHUNK, 256),
+    for k, v in ((hippt.OPT_WAVE_THRESHOLD, 32), (hippt.OPT_SCRATCH_MB, 32768), (hippt.OPT_CHUNK, 256),
                  (hippt.OPT_COUNT_TRAVERSAL, 0), (hippt.OPT_BLOCKS_PER_CU, 0), (hippt.OPT_LDS_SCENE, 1),
                  (hippt.OPT_PATH_MODE, 0), (hippt.OPT_WAVEFRONT_SLOTS, 1 << 24), (hippt.OPT_LEAF_EXIT, -1),
                  (hippt.OPT_NODE_EXIT, -1), (hippt.OPT_BVH_SAH, 1), (hippt.OPT_BVH_WIDTH, 0),
-                 (hippt.OPT_STACK_CAP, 0)):
+                 (hippt.OPT_STACK_CAP, 0), (hippt.OPT_BVH_QUANT, -1)):
         t.setOption(k, v)
     t.resetStats()
     yield t
@@ -248,17 +248,19 @@ def test_loop_exits_do_not_change_results(pt, name, mode):
 @pytest.mark.parametrize("name", ["blob70k", "cornell34", "random_scene", "cornell_mixed"])
 def test_bvh_width_and_stack_spill_do_not_change_results(pt, name):
     """The 4-wide tree (HIPPT_OPT_BVH_WIDTH 4, with the LDS stack capped at 4 entries so deep
-    traversals spill to the global spill area and refill) and the 2-wide tree give the
-    oracle's image bit for bit; the LDS-resident and global-memory scene paths alike."""
+    traversals spill to the global spill area and refill; float and 8-bit child boxes) and the
+    2-wide tree give the oracle's image bit for bit; the LDS-resident and global-memory scene
+    paths alike."""
     sc = scenes.get_scene(name)
     pt.uploadMesh(sc)
     w, h = (40, 24) if name == "random_scene" else (56, 40)
     ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
     for lds in (1, 0):
         pt.setOption(hippt.OPT_LDS_SCENE, lds)
-        for width, cap in ((2, 0), (0, 0), (4, 0), (4, 4), (4, 7)):
+        for width, cap, quant in ((2, 0, -1), (0, 0, -1), (4, 0, 0), (4, 0, 1), (4, 4, 1), (4, 7, 0)):
             pt.setOption(hippt.OPT_BVH_WIDTH, width)
             pt.setOption(hippt.OPT_STACK_CAP, cap)
+            pt.setOption(hippt.OPT_BVH_QUANT, quant)
             assert pt.initialize(w, h)
             assert pt.renderFrames(3, 8)
             got = pt.readback()

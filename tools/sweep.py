@@ -26,7 +26,8 @@ KEYS = {"wave": hippt.OPT_WAVE_THRESHOLD, "chunk": hippt.OPT_CHUNK, "scratch": h
         "slots": hippt.OPT_WAVEFRONT_SLOTS, "leaf": hippt.OPT_BVH_LEAF, "tcost": hippt.OPT_BVH_TRAVERSAL_COST,
         "depth": hippt.OPT_BVH_MAX_DEPTH, "leafexit": hippt.OPT_LEAF_EXIT,
         "nodeexit": hippt.OPT_NODE_EXIT, "sah": hippt.OPT_BVH_SAH,
-        "width": hippt.OPT_BVH_WIDTH, "stackcap": hippt.OPT_STACK_CAP}
+        "width": hippt.OPT_BVH_WIDTH, "stackcap": hippt.OPT_STACK_CAP,
+        "quant": hippt.OPT_BVH_QUANT}
 REUPLOAD = {"leaf", "tcost", "depth", "sah"}  # build parameters: take effect at the next upload
 
 
