@@ -19,7 +19,8 @@ Also reported on rank 0:
                 visit (112 B per 4-wide visit),
                 48 B per triangle test, 32 B per shaded hit, 12 B per sample written
                 (DESIGN.md §Roofline).  traffic = PMC-measured HBM bytes per launch from
-                profiles/ when a matching summary exists, else null.
+                profiles/ when a matching summary exists, else null; limiters = that
+                summary's VALU issue / texture-addresser busy fractions.
   cpu_baseline  the reference CPU path tracer (RayTracer.h + Qt-free RenderWorker, built as
                 oracle/_ref/ref_harness) timed on this box's host cores over a bounded row
                 sample of the same workload.
@@ -148,7 +149,8 @@ def load_pmc(args, workload: str):
         except (OSError, ValueError):
             continue
         if d.get("workload") == workload:
-            return d.get("hbm_bytes_per_launch")
+            d["source"] = os.path.relpath(path, REPO)
+            return d
     return None
 
 
@@ -262,7 +264,8 @@ def main():
     workload = f"{args.scene} {args.width}x{args.height} {args.spp}spp depth{args.depth}"
     if args.path_mode == "wavefront":
         workload += " wavefront"
-    traffic = load_pmc(args, workload)
+    pmc = load_pmc(args, workload)
+    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
 
     if rank == 0:
         cpu = cpu_baseline(args, scene) if world == 1 else None
@@ -305,6 +308,11 @@ def main():
                 "launches_per_step": launches,
                 "alg_bytes_per_launch": int(alg_bytes_launch),
                 "node_visits_per_step": counted["nodeVisits"], "tri_tests_per_step": counted["triTests"],
+                # what the profile of this workload says bounds the kernel (not HBM: the scene is
+                # cache-resident): VALU issue and the vector-memory address unit (TA)
+                "limiters": {k: pmc.get(k) for k in ("source", "valu_issue_busy", "valu_lane_utilization",
+                                                     "ta_busy", "hbm_gbs", "mean_launch_ms_rocprof")}
+                if pmc else None,
                 "valu": {"achieved": round(flops_launch / (mean_launch_ms * 1e-3) / 1e12, 3) if mean_launch_ms else 0.0,
                          "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                          "frac": round(flops_launch / (mean_launch_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4)

@@ -5,7 +5,7 @@ TAG=${1:?tag}
 mkdir -p gpurun_out/$TAG
 B="timeout -k 10 300 python3 bench.py"
 $B > gpurun_out/$TAG/cornell.json 2> gpurun_out/$TAG/cornell.err
-$B --scene blob70k --cpu-baseline off > gpurun_out/$TAG/blob.json 2>> gpurun_out/$TAG/err
+$B --scene blob70k > gpurun_out/$TAG/blob.json 2>> gpurun_out/$TAG/err
 $B --scene blob70k --width 3840 --height 2160 --spp 256 --steps 2 --warmup 1 --cpu-baseline off > gpurun_out/$TAG/blob4k.json 2>> gpurun_out/$TAG/err
 $B --scene blob70k --path-mode wavefront --cpu-baseline off > gpurun_out/$TAG/blob_wf.json 2>> gpurun_out/$TAG/err
 $B --scene random_scene --cpu-baseline off > gpurun_out/$TAG/random.json 2>> gpurun_out/$TAG/err
