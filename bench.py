@@ -4,9 +4,12 @@
 Workload (BASELINE.json configs[1]): Cornell-34 scene, 1920x1080, 64 spp, 8 bounces.
 One step = the whole workload once: 64 frames of every pixel (running-average accumulation,
 frames 0..63) through libhippt's C ABI.  With N GPUs (torchrun, one process per GPU) rank r
-renders rows r, r+N, r+2N, ... (interleaved: contiguous bands differ in cost by up to 1.6x; the
-image is fixed, strong scaling); no collective touches the data path — ranks only meet at the barriers and the max-over-ranks
-of the timed interval (gloo, CPU).
+renders rows r, r+N, r+2N, ... (interleaved: contiguous bands differ in cost by up to 1.6x) and
+the image is bit-identical for any N.  --scaling weak (default): the step renders 64*N frames
+of the 1080p image (frames 0..64N-1, a progressive render whose sample count grows with the
+GPUs), so every rank traces as many samples as one GPU does alone; --scaling strong: 64
+frames at every N (each rank a 1/N share of a fixed job).  No collective touches the data
+path — ranks only meet at the barriers and the max-over-ranks of the timed interval (gloo, CPU).
 
 value = segments traced by all ranks in the K timed steps / max-over-ranks wall time, in
 millions per second; the segment count is the exact count the kernel accumulates (one per
@@ -63,6 +66,8 @@ def parse():
     p.add_argument("--path-mode", default="megakernel", choices=["megakernel", "wavefront"],
                    help="BASELINE configs[4] A/B: persistent megakernel or wavefront kernels")
     p.add_argument("--wavefront-slots", type=int, default=None)
+    p.add_argument("--scaling", default="weak", choices=["weak", "strong"],
+                   help="N GPUs render N*spp frames (weak: fixed work per GPU) or spp frames (strong)")
     p.add_argument("--split", default="interleave", choices=["interleave", "bands"],
                    help="rows per rank for N>1: interleaved (rank r: rows r, r+N, ...) or contiguous bands")
     p.add_argument("--width", type=int, default=1920)
@@ -164,7 +169,16 @@ def main():
 
     rank, local_rank, world = hd.env_rank()
     if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # gloo prints its peer-connection notice on stdout; keep stdout to the one JSON line
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     if world != args.gpus:
         log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     lib = hippt.load_library()
@@ -209,10 +223,12 @@ def main():
     if not pt.initialize(args.width, args.height):
         raise SystemExit(pt.lastError())
 
+    frames = args.spp * world if args.scaling == "weak" else args.spp
+
     def step():
-        # frames 0..spp-1: frame 0 overwrites the accumulation (acc*0 + L), so every step is
+        # frames 0..frames-1: frame 0 overwrites the accumulation (acc*0 + L), so every step is
         # the identical full workload
-        if not pt._lib.hipptRenderFramesAsync(0, args.spp, args.depth, None):
+        if not pt._lib.hipptRenderFramesAsync(0, frames, args.depth, None):
             raise SystemExit(hippt.load_library().hipptLastError().decode())
 
     # counted pass (untimed): traversal counters for the roofline's algorithmic bytes
@@ -261,7 +277,7 @@ def main():
                     + FLOP_SHADE * counted["segments"]) / launches
     mean_launch_ms = st["traceMs"] / max(1, st["traceLaunches"])
     achieved = alg_bytes_launch / (mean_launch_ms * 1e-3) / 1e9 if mean_launch_ms > 0 else 0.0
-    workload = f"{args.scene} {args.width}x{args.height} {args.spp}spp depth{args.depth}"
+    workload = f"{args.scene} {args.width}x{args.height} {frames}spp depth{args.depth}"
     if args.path_mode == "wavefront":
         workload += " wavefront"
     pmc = load_pmc(args, workload)
@@ -279,16 +295,18 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed_max * 1e3 / args.steps, 4),
             "higher_is_better": True,
-            "scaling": "strong",
+            "scaling": args.scaling,
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic",
             "config": {
-                "workload": workload + " (BASELINE configs[1])" if args.scene == "cornell34" and args.width == 1920
-                and args.height == 1080 and args.spp == 64 and args.depth == 8 else workload,
+                "workload": workload + (" (BASELINE configs[1])" if world == 1 or args.scaling == "strong"
+                                        else " (BASELINE configs[1] per GPU)")
+                if args.scene == "cornell34" and args.width == 1920 and args.height == 1080 and args.spp == 64
+                and args.depth == 8 else workload,
                 "scene": args.scene, "triangles": scene.num_tris, "spheres": scene.num_spheres,
                 "path_mode": args.path_mode, "width": args.width, "height": args.height,
-                "spp": args.spp, "max_depth": args.depth,
+                "spp": frames, "spp_per_gpu_share": args.spp, "max_depth": args.depth,
                 "parallelism": f"{'interleaved-rows' if args.split == 'interleave' else 'row-bands'} x{world}",
                 "segments_per_step": segments // max(1, args.steps),
                 "pixel_samples_per_step": samples // max(1, args.steps),

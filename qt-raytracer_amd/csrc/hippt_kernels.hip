@@ -184,8 +184,11 @@ __device__ unsigned long long g_timeline[65536 * 6];
 #endif
 #define HIPPT_SGPR_ATTR __attribute__((amdgpu_num_sgpr(HIPPT_NUM_SGPR)))
 
+#ifndef HIPPT_WIDE_WAVES_PER_EU
+#define HIPPT_WIDE_WAVES_PER_EU 7
+#endif
 template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE, bool QUANT>
-__global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? 7 : HIPPT_MESH_WAVES_PER_EU) HIPPT_SGPR_ATTR void mesh_kernel(MeshParams P) {
+__global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_EU : HIPPT_MESH_WAVES_PER_EU) HIPPT_SGPR_ATTR void mesh_kernel(MeshParams P) {
     static_assert(!QUANT || (WIDE && !LDS_SCENE), "quantized nodes: 4-wide global-memory traversal only");
 #ifdef HIPPT_DEBUG_TIMELINE
     const unsigned tlw = blockIdx.x * 4u + (threadIdx.x >> 6);
