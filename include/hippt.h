@@ -179,7 +179,8 @@ int hipptGetCounters(unsigned long long *out, int n);
 
 enum {
     HIPPT_OPT_COUNT_TRAVERSAL = 1,  /* 1: count node visits / triangle tests (slower) */
-    HIPPT_OPT_WAVE_THRESHOLD = 2,   /* lanes still traversing below which a wave goes to shade */
+    HIPPT_OPT_WAVE_THRESHOLD = 2,   /* lanes still traversing below which a wave goes to shade; -1 (default):
+                                       16 for LDS-resident scenes, 32 otherwise */
     HIPPT_OPT_SCRATCH_MB = 3,       /* cap of the per-batch sample scratch per device (32768: one batch for 4K x 256 spp) */
     HIPPT_OPT_CHUNK = 4,            /* work items a wave takes from the global queue at once */
     HIPPT_OPT_BLOCKS_PER_CU = 5,    /* persistent-grid residency (0 = occupancy query) */

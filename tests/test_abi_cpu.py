@@ -76,7 +76,8 @@ def test_options_validate():
     assert not lib.hipptSetOption(hippt.OPT_WAVE_THRESHOLD, 65)
     assert not lib.hipptSetOption(hippt.OPT_CHUNK, 100)
     assert not lib.hipptSetOption(999, 1)
-    assert lib.hipptSetOption(hippt.OPT_WAVE_THRESHOLD, 16)
+    assert lib.hipptSetOption(hippt.OPT_WAVE_THRESHOLD, -1)
+    assert not lib.hipptSetOption(hippt.OPT_WAVE_THRESHOLD, -2)
 
 
 def test_mesh_upload_validates_inputs():

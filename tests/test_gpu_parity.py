@@ -23,7 +23,7 @@ def pt():
     t.setRowRange(0, 0)
     t.setOption(hippt.OPT_DEVICE_ROWS, 1)
     t.useBuiltinScene(hippt.SCENE_SPHERE4)
-    for k, v in ((hippt.OPT_WAVE_THRESHOLD, 32), (hippt.OPT_SCRATCH_MB, 32768), (hippt.OPT_CHUNK, 256),
+    for k, v in ((hippt.OPT_WAVE_THRESHOLD, -1), (hippt.OPT_SCRATCH_MB, 32768), (hippt.OPT_CHUNK, 256),
                  (hippt.OPT_COUNT_TRAVERSAL, 0), (hippt.OPT_BLOCKS_PER_CU, 0), (hippt.OPT_LDS_SCENE, 1),
                  (hippt.OPT_PATH_MODE, 0), (hippt.OPT_WAVEFRONT_SLOTS, 1 << 24), (hippt.OPT_LEAF_EXIT, -1),
                  (hippt.OPT_NODE_EXIT, -1), (hippt.OPT_BVH_SAH, 1), (hippt.OPT_BVH_WIDTH, 0),
@@ -366,11 +366,13 @@ def test_mesh_depth_zero_is_black(pt):
     assert np.all(px == 0xFF000000) and np.all(acc[..., :3] == 0) and pt.stats()["segments"] == 0
 
 
-def test_full_size_1080p_rows_and_determinism(pt):
-    """BASELINE config 2 size: bit-exact on sampled rows, deterministic, counts consistent."""
-    sc = scenes.cornell34()
+@pytest.mark.parametrize("name,w,h,spp", [("cornell34", 1920, 1080, 8), ("blob70k", 1920, 1080, 4),
+                                           ("blob70k", 3840, 2160, 2)])
+def test_full_size_1080p_rows_and_determinism(pt, name, w, h, spp):
+    """BASELINE config 2/3/4 sizes (LDS 4-wide tree; global 8-bit 4-wide tree): bit-exact on
+    sampled rows, deterministic, counts consistent."""
+    sc = scenes.get_scene(name)
     pt.uploadMesh(sc)
-    w, h, spp = 1920, 1080, 8
     assert pt.initialize(w, h)
     assert pt.renderFrames(spp, 8)
     a = pt.readback()
@@ -381,8 +383,8 @@ def test_full_size_1080p_rows_and_determinism(pt):
     assert pt.renderFrames(spp, 8)
     b = pt.readback()
     _assert_same(a[0], a[1], b[0], b[1])
-    ms = po.MeshScene(sc, w, h)
-    for y0 in (0, 537, 1078):
+    ms = po.MeshScene(sc, w, h, accel=1)
+    for y0 in (0, h // 2 - 3, h - 2):
         ora = ms.frames(0, spp, 8, y0=y0, y1=y0 + 2)
         _assert_same(a[0][y0:y0 + 2], a[1][y0:y0 + 2], ora[0], ora[1])
 
