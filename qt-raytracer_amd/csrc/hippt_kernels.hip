@@ -164,8 +164,8 @@ __global__ __launch_bounds__(256) void sphere4_kernel(Sphere4Params P) {
 // 16 distinct 4-bank groups, so ds_read_b128 of different nodes in a lane group do not
 // conflict), primitives at 48 bytes (12 dwords, likewise), shading records at 16 bytes.
 constexpr int kLdsNodeF4 = 5;
-// 4-wide nodes in LDS: the 7 float4 in use (boxes + codes) at a 112-byte stride.
-constexpr int kLdsNode4F4 = 7;
+// 4-wide nodes in LDS: the global 128-byte layout (row addresses by or/xor of the octant offsets).
+constexpr int kLdsNode4F4 = 8;
 
 #ifdef HIPPT_DEBUG_TIMELINE
 // per wave: [0] start, [1] first drained fetch, [2] end (s_memrealtime, 100 MHz), [3] items,
@@ -212,8 +212,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         float4 *sTris = sNodes + P.numNodes * ldsNodeF4;
         float4 *sShade = sTris + P.numTris * 3;
         if (WIDE) {
-            for (int i = threadIdx.x; i < P.numNodes * kLdsNode4F4; i += kMeshBlock)
-                sNodes[i] = P.nodes[(i / kLdsNode4F4) * 8 + i % kLdsNode4F4];
+            for (int i = threadIdx.x; i < P.numNodes * kLdsNode4F4; i += kMeshBlock) sNodes[i] = P.nodes[i];
         } else {
             for (int i = threadIdx.x; i < P.numNodes * 4; i += kMeshBlock)
                 sNodes[(i >> 2) * kLdsNodeF4 + (i & 3)] = P.nodes[i];
@@ -243,7 +242,10 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     T.bestO = 0x7fffffff;
     float tr = 1, tg = 1, tb = 1;
     bool need = true;
-    unsigned long long segs = 0, samples = 0, nvis = 0, ntest = 0;
+    // per-lane counts fit 32 bits (a lane traces a few thousand segments per launch); widened
+    // for the wave sum
+    unsigned segs = 0, samples = 0;
+    unsigned long long nvis = 0, ntest = 0;
     unsigned pc[16] = {0};
 
     for (;;) {
@@ -313,15 +315,14 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         g_timeline[6 * tlw + 3] = tlItems;
     }
 #endif
-    segs = wave_sum(segs);
-    samples = wave_sum(samples);
+    const unsigned long long segsW = wave_sum(segs), samplesW = wave_sum(samples);
     if (STATS) {
         nvis = wave_sum(nvis);
         ntest = wave_sum(ntest);
     }
     if (__lane_id() == 0) {
-        atomicAdd(&P.stats[0], segs);
-        atomicAdd(&P.stats[1], samples);
+        atomicAdd(&P.stats[0], segsW);
+        atomicAdd(&P.stats[1], samplesW);
         if (STATS) {
             atomicAdd(&P.stats[2], nvis);
             atomicAdd(&P.stats[3], ntest);

@@ -615,7 +615,8 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
                                                     unsigned long long &ntest, unsigned *pc, unsigned leafExit,
                                                     unsigned nodeExit, const SpillArea &S) {
     const float tmin = 0.001f;
-    const unsigned sx = near_row(r.ix), sy = near_row(r.iy), sz = near_row(r.iz);
+    // near-row byte offsets of this ray's octant within a node (x at 0/16, y at 32/48, z at 64/80)
+    const unsigned sx = near_row(r.ix), sy = near_row(r.iy) | 32u, sz = near_row(r.iz) | 64u;
     while (T.cur >= 0) {
         prof<STATS>(pc, 3);
         // rows lo.x hi.x lo.y hi.y lo.z hi.z: read as near/far rows of this ray's octant (32-bit
@@ -624,12 +625,11 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
         unsigned k0, k1, k2, k3;
         int4 ch;
         if (!QUANT) {
-            const float4 nx = ld4(nodes, nb + sx);
-            const float4 fx = ld4(nodes, nb + (sx ^ 16u));
-            const float4 ny = ld4(nodes, nb + sy + 32u);
-            const float4 fy = ld4(nodes, nb + (sy ^ 16u) + 32u);
-            const float4 nz = ld4(nodes, nb + sz + 64u);
-            const float4 fz = ld4(nodes, nb + (sz ^ 16u) + 64u);
+            // 128-byte float nodes (NODE_F4 == 8, LDS and global): nb's low 7 bits are zero
+            const unsigned ax = nb | sx, ay = nb | sy, az = nb | sz;  // near rows; far = near ^ 16
+            const float4 nx = ld4(nodes, ax), fx = ld4(nodes, ax ^ 16u);
+            const float4 ny = ld4(nodes, ay), fy = ld4(nodes, ay ^ 16u);
+            const float4 nz = ld4(nodes, az), fz = ld4(nodes, az ^ 16u);
             ch = *reinterpret_cast<const int4 *>(reinterpret_cast<const char *>(nodes) + nb + 96u);
             k0 = child_key(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, r, tmin, T.bestT);
             k1 = child_key(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, r, tmin, T.bestT);
@@ -646,9 +646,10 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
             const float by = q2.z * r.iy, ay = fmaf(o.y, r.iy, -r.oiy);
             const float bz = q2.w * r.iz, az = fmaf(o.z, r.iz, -r.oiz);
             const unsigned qlz = __float_as_uint(q2.x), qhz = __float_as_uint(q2.y);
-            const unsigned nxw = sx ? q.y : q.x, fxw = sx ? q.x : q.y;
-            const unsigned nyw = sy ? q.w : q.z, fyw = sy ? q.z : q.w;
-            const unsigned nzw = sz ? qhz : qlz, fzw = sz ? qlz : qhz;
+            const bool mx = sx & 16u, my_ = sy & 16u, mz = sz & 16u;
+            const unsigned nxw = mx ? q.y : q.x, fxw = mx ? q.x : q.y;
+            const unsigned nyw = my_ ? q.w : q.z, fyw = my_ ? q.z : q.w;
+            const unsigned nzw = mz ? qhz : qlz, fzw = mz ? qlz : qhz;
             k0 = child_key_q<0>(nxw, fxw, nyw, fyw, nzw, fzw, ax, bx, ay, by, az, bz, tmin, T.bestT);
             k1 = child_key_q<1>(nxw, fxw, nyw, fyw, nzw, fzw, ax, bx, ay, by, az, bz, tmin, T.bestT);
             k2 = child_key_q<2>(nxw, fxw, nyw, fyw, nzw, fzw, ax, bx, ay, by, az, bz, tmin, T.bestT);
