@@ -656,8 +656,8 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
             k3 = child_key_q<3>(nxw, fxw, nyw, fyw, nzw, fzw, ax, bx, ay, by, az, bz, tmin, T.bestT);
         }
         if (STATS) ++nvis;
-        const int nh = int(k0 != 0xffffffffu) + int(k1 != 0xffffffffu) + int(k2 != 0xffffffffu) +
-                       int(k3 != 0xffffffffu);
+        // hit children: a miss key is all ones (bit 31), a hit key a positive float's bits
+        const int nh = 4 - int((k0 >> 31) + (k1 >> 31) + (k2 >> 31) + (k3 >> 31));
         // sorting network (0,1)(2,3)(0,2)(1,3)(1,2), codes carried along: c0 nearest
         int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
         cas(k0, c0, k1, c1);
