@@ -197,8 +197,8 @@ enum {
                                        (0 = never); -1 (default): 48 */
     , HIPPT_OPT_BVH_SAH = 16        /* BVH split search: 1 (default) all axes, exact sweep SAH (32 bins on
                                        nodes over 65536 primitives); 0: 16 bins on the longest axis; next upload */
-    , HIPPT_OPT_BVH_WIDTH = 17      /* megakernel traversal over the 4-wide (4) or 2-wide (2) BVH; 0 (default):
-                                       4-wide (the wavefront path always traverses the 2-wide tree) */
+    , HIPPT_OPT_BVH_WIDTH = 17      /* traversal over the 4-wide (4) or 2-wide (2) BVH (megakernel and wavefront);
+                                       0 (default): 4-wide */
     , HIPPT_OPT_STACK_CAP = 18      /* 4-wide traversal: LDS stack entries per lane, 4..30 (deeper stacks spill
                                        to global memory); 0 (default): the tree's bound, at most 19 (30 for
                                        LDS scenes) */

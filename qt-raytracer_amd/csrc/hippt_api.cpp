@@ -392,10 +392,28 @@ long long occupancy_key(int version, int stackDepth, bool lds, bool full, bool w
            (full ? 1 : 0);
 }
 
+// 4-wide traversal of a tree whose stack bound exceeds the LDS capacity: a per-lane spill
+// area of spillCap entries for every lane of a `blocks`-block persistent grid.
+bool ensure_spill(Ctx &c, hippt::MeshParams &p, long long blocks, bool spills, int spillCap, const char **err) {
+    if (!spills) return true;
+    p.spillCap = spillCap;
+    const size_t bytes = size_t(blocks) * hippt::kMeshBlock * size_t(spillCap) * sizeof(int);
+    if (c.spillBytes < bytes) {
+        HIP_TRY(hipStreamSynchronize(c.stream));
+        (void)hipFree(c.spill);
+        c.spill = nullptr;
+        c.spillBytes = 0;
+        HIP_TRY(hipMalloc(&c.spill, bytes));
+        c.spillBytes = bytes;
+    }
+    p.spill = c.spill;
+    return true;
+}
+
 // Wavefront variant (hippt_wavefront.hip): init + generate, then extend/shade/generate
 // iterations until the ray queue stays empty.  The host reads the queue size with one batch of
 // lag (pinned snapshot + event), so the call returns within ~16 iterations of the end.
-bool run_wavefront(Ctx &c, const hippt::MeshParams &p, bool cnt, const char **err) {
+bool run_wavefront(Ctx &c, hippt::MeshParams p, bool cnt, bool spills, int spillCap, const char **err) {
     State &s = S();
     const unsigned slots = std::max(64u, std::min(s.wfSlots, std::max(64u, p.totalItems)));
     unsigned shardCap = 0;
@@ -421,15 +439,18 @@ bool run_wavefront(Ctx &c, const hippt::MeshParams &p, bool cnt, const char **er
     W.extQ0 = queues;
     W.extQ1 = queues + size_t(hippt::kWfShards) * shardCap;
     W.genQ = queues + 2 * size_t(hippt::kWfShards) * shardCap;
-    const long long occKey = occupancy_key(s.scene.version, p.stackDepth, p.ldsScene != 0, p.full != 0);
+    const bool wide = p.wide != 0, quant = p.wide == 2;
+    const long long occKey = occupancy_key(s.scene.version, p.stackDepth, p.ldsScene != 0, p.full != 0, wide, quant);
     if (c.wfOccKey != occKey) {
         const int ln = p.ldsScene ? p.numNodes : 0, lt = p.ldsScene ? p.numTris : 0;
-        c.wfBlocksPerCu[0] = hippt::wf_extend_blocks_per_cu(false, p.full != 0, p.stackDepth, ln, lt);
-        c.wfBlocksPerCu[1] = hippt::wf_extend_blocks_per_cu(true, p.full != 0, p.stackDepth, ln, lt);
+        c.wfBlocksPerCu[0] = hippt::wf_extend_blocks_per_cu(false, p.full != 0, wide, quant, p.stackDepth, ln, lt);
+        c.wfBlocksPerCu[1] = hippt::wf_extend_blocks_per_cu(true, p.full != 0, wide, quant, p.stackDepth, ln, lt);
         c.wfOccKey = occKey;
     }
     const int bpc = s.blocksPerCu > 0 ? s.blocksPerCu : c.wfBlocksPerCu[cnt ? 1 : 0];
     const int blocks = int(std::max(1LL, std::min<long long>((long long)c.cus * bpc, (slots + 255) / 256)));
+    if (!ensure_spill(c, p, blocks, spills, spillCap, err)) return false;
+    W.mp = p;
     EventPair ev;
     if (!next_events(c, ev, err)) return false;
     HIP_TRY(hipEventRecord(ev.a, c.stream));
@@ -526,12 +547,12 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                     c.scratchBytes = need;
                 }
                 const bool cnt = s.countTraversal;
-                // Megakernel traversal over the 4-wide tree (HIPPT_OPT_BVH_WIDTH; wavefront: 2-wide).
+                // Traversal over the 4-wide tree (HIPPT_OPT_BVH_WIDTH), megakernel and wavefront.
                 // Automatic: 4-wide.  With near/far rows read by the ray's octant, 4-wide beats
                 // 2-wide on LDS scenes (Cornell 31.7 -> 35.3 G) and on global-memory trees (blob70k
                 // 14.2 -> 15.4 G: half the dependent node fetches, 18% fewer load instructions);
                 // random_scene (spheres, general kernel) 20.6 vs 20.5 G.
-                const bool wide = s.pathMode == 0 && s.scene.numNodes4 > 0 && s.bvhWidth != 2;
+                const bool wide = s.scene.numNodes4 > 0 && s.bvhWidth != 2;
                 s.activeWidth = wide ? 4 : 2;
                 const int numNodes = wide ? s.scene.numNodes4 : s.scene.numNodes, numTris = s.scene.numTris;
                 // small scenes live in LDS (scene bytes beyond the stack under the limit)
@@ -610,24 +631,12 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.wide = quant ? 2 : wide ? 1 : 0;
                         p.stackCap = stackCap;
                         if (s.pathMode == 1) {
-                            if (!run_wavefront(c, p, cnt, err)) return false;
+                            if (!run_wavefront(c, p, cnt, spills, s.scene.stackBound4 + 3, err)) return false;
                         } else {
                             long long blocks = (long long)c.cus * bpc;
                             blocks = std::min<long long>(blocks, (total + hippt::kMeshBlock - 1) / hippt::kMeshBlock);
                             blocks = std::max<long long>(blocks, 1);
-                            if (spills) {
-                                p.spillCap = s.scene.stackBound4 + 3;
-                                const size_t bytes = size_t(blocks) * hippt::kMeshBlock * size_t(p.spillCap) * sizeof(int);
-                                if (c.spillBytes < bytes) {
-                                    HIP_TRY(hipStreamSynchronize(c.stream));
-                                    (void)hipFree(c.spill);
-                                    c.spill = nullptr;
-                                    c.spillBytes = 0;
-                                    HIP_TRY(hipMalloc(&c.spill, bytes));
-                                    c.spillBytes = bytes;
-                                }
-                                p.spill = c.spill;
-                            }
+                            if (!ensure_spill(c, p, blocks, spills, s.scene.stackBound4 + 3, err)) return false;
                             HIP_TRY(hipMemsetAsync(c.queue, 0, kQueueBytes, c.stream));
                             EventPair ev;
                             if (!next_events(c, ev, err)) return false;

@@ -97,7 +97,8 @@ __global__ void wf_init(WfParams W) {
     if (i == 0) W.ctr[ctr_word(kCtrWork)] = 0;
 }
 
-template <bool STATS, bool LDS_SCENE, bool FULL>
+// WIDE: the megakernel's 4-wide traversal (QUANT: over 8-bit child boxes, global memory only).
+template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE, bool QUANT>
 __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
     extern __shared__ int stk[];
     int *const my = stk + threadIdx.x;
@@ -116,15 +117,22 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
         }
     }
     const float4 *nodes = P.nodes, *tris = P.tris;
+    constexpr int ldsNodeF4 = WIDE ? 8 : 5;  // mesh_lds_bytes layout
     if (LDS_SCENE) {
         float4 *sNodes = reinterpret_cast<float4 *>(stk + (P.stackDepth + 1) * kMeshBlock);
-        float4 *sTris = sNodes + P.numNodes * 5;
-        for (int i = threadIdx.x; i < P.numNodes * 4; i += kMeshBlock) sNodes[(i >> 2) * 5 + (i & 3)] = P.nodes[i];
+        float4 *sTris = sNodes + P.numNodes * ldsNodeF4;
+        if (WIDE) {
+            for (int i = threadIdx.x; i < P.numNodes * 8; i += kMeshBlock) sNodes[i] = P.nodes[i];
+        } else {
+            for (int i = threadIdx.x; i < P.numNodes * 4; i += kMeshBlock) sNodes[(i >> 2) * 5 + (i & 3)] = P.nodes[i];
+        }
         for (int i = threadIdx.x; i < P.numTris * 3; i += kMeshBlock) sTris[i] = P.tris[i];
         __syncthreads();
         nodes = sNodes;
         tris = sTris;
     }
+    constexpr int nodeF4 = WIDE ? (QUANT ? 4 : 8) : (LDS_SCENE ? 5 : 4);
+    const SpillArea S{P.spill, (blockIdx.x * unsigned(kMeshBlock) + threadIdx.x) * unsigned(P.spillCap), P.stackCap};
     const unsigned *queue = cur ? W.extQ1 : W.extQ0;
     // each wave drains its block's home shard first, then the others in turn (one fetch
     // counter per shard spreads the atomics over kWfShards lines)
@@ -164,7 +172,11 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
         need = false;
         if (!__any(busy(T))) break;
         do {
-            traverse_round<LDS_SCENE ? 5 : 4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
+            if (WIDE)
+                traverse_round_wide<nodeF4, STATS, FULL, QUANT>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit,
+                                                                P.nodeExit, S);
+            else
+                traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
         } while (__popcll(__ballot(busy(T))) > unsigned(P.waveThreshold));
         if (slot != kNone && !busy(T)) {
             *reinterpret_cast<float2 *>(W.st + 4 * size_t(slot) + 3) = make_float2(T.bestT, __int_as_float(T.bestI));
@@ -266,13 +278,15 @@ __global__ __launch_bounds__(kWfBlock) void wf_generate(WfParams W, int nxt, int
 }
 
 using ExtFn = void (*)(WfParams, int);
-ExtFn ext_fn(bool count, bool lds, bool full) {
-    if (full) {
-        if (count) return lds ? wf_extend<true, true, true> : wf_extend<true, false, true>;
-        return lds ? wf_extend<false, true, true> : wf_extend<false, false, true>;
-    }
-    if (count) return lds ? wf_extend<true, true, false> : wf_extend<true, false, false>;
-    return lds ? wf_extend<false, true, false> : wf_extend<false, false, false>;
+template <bool STATS, bool FULL>
+ExtFn ext_fn_fmt(bool lds, bool wide, bool quant) {
+    if (lds) return wide ? wf_extend<STATS, true, FULL, true, false> : wf_extend<STATS, true, FULL, false, false>;
+    if (!wide) return wf_extend<STATS, false, FULL, false, false>;
+    return quant ? wf_extend<STATS, false, FULL, true, true> : wf_extend<STATS, false, FULL, true, false>;
+}
+ExtFn ext_fn(bool count, bool lds, bool full, bool wide, bool quant) {
+    if (count) return full ? ext_fn_fmt<true, true>(lds, wide, quant) : ext_fn_fmt<true, false>(lds, wide, quant);
+    return full ? ext_fn_fmt<false, true>(lds, wide, quant) : ext_fn_fmt<false, false>(lds, wide, quant);
 }
 
 }  // namespace
@@ -302,8 +316,9 @@ hipError_t wf_launch_generate(const WfParams &W, int nxt, bool countSamples, hip
 hipError_t wf_launch_extend(const WfParams &W, int cur, int blocks, bool countTraversal, hipStream_t s) {
     const MeshParams &P = W.mp;
     const bool lds = P.ldsScene != 0;
-    const size_t bytes = mesh_lds_bytes(P.stackDepth, lds ? P.numNodes : 0, lds ? P.numTris : 0, false);
-    hipLaunchKernelGGL(ext_fn(countTraversal, lds, P.full != 0), dim3(blocks), dim3(kMeshBlock), bytes, s, W, cur);
+    const size_t bytes = mesh_lds_bytes(P.stackDepth, lds ? P.numNodes : 0, lds ? P.numTris : 0, P.wide != 0);
+    hipLaunchKernelGGL(ext_fn(countTraversal, lds, P.full != 0, P.wide != 0, P.wide == 2 && !lds), dim3(blocks),
+                       dim3(kMeshBlock), bytes, s, W, cur);
     return hipGetLastError();
 }
 
@@ -312,10 +327,12 @@ hipError_t wf_launch_shade(const WfParams &W, int cur, hipStream_t s) {
     return hipGetLastError();
 }
 
-int wf_extend_blocks_per_cu(bool countTraversal, bool full, int stackDepth, int ldsNodes, int ldsTris) {
+int wf_extend_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,
+                            int ldsTris) {
     int n = 0;
-    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, false);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, ext_fn(countTraversal, ldsNodes > 0, full), kMeshBlock, bytes) !=
+    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, wide);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
+            &n, ext_fn(countTraversal, ldsNodes > 0, full, wide, quant && wide && ldsNodes == 0), kMeshBlock, bytes) !=
             hipSuccess ||
         n <= 0)
         n = 1;

@@ -102,19 +102,23 @@ def test_mesh_matches_oracle(pt, name, w, h, spp, depth):
     assert st["segments"] == segs and st["pixelSamples"] == samples
 
 
-@pytest.mark.parametrize("name,w,h,spp,depth,slots", [
-    ("cornell34", 96, 64, 8, 8, 1 << 21),
-    ("cornell34", 33, 17, 3, 4, 64),
-    ("blob70k", 64, 48, 4, 8, 1000),
-    ("blob70k", 20, 11, 2, 1, 100),
+@pytest.mark.parametrize("name,w,h,spp,depth,slots,width,cap", [
+    ("cornell34", 96, 64, 8, 8, 1 << 21, 0, 0),
+    ("cornell34", 33, 17, 3, 4, 64, 2, 0),
+    ("blob70k", 64, 48, 4, 8, 1000, 0, 0),
+    ("blob70k", 64, 48, 4, 8, 5000, 0, 6),
+    ("blob70k", 20, 11, 2, 1, 100, 2, 0),
 ])
-def test_wavefront_matches_oracle(pt, name, w, h, spp, depth, slots):
+def test_wavefront_matches_oracle(pt, name, w, h, spp, depth, slots, width, cap):
     """The wavefront variant (BASELINE config 5) is bit-identical to the oracle/megakernel,
-    including with a path pool much smaller than the work (many regenerate rounds)."""
+    including with a path pool much smaller than the work (many regenerate rounds), over the
+    2-wide and the 4-wide trees (a small LDS stack cap forces spills to the global area)."""
     sc = scenes.get_scene(name)
     pt.uploadMesh(sc)
     pt.setOption(hippt.OPT_PATH_MODE, 1)
     pt.setOption(hippt.OPT_WAVEFRONT_SLOTS, slots)
+    pt.setOption(hippt.OPT_BVH_WIDTH, width)
+    pt.setOption(hippt.OPT_STACK_CAP, cap)
     assert pt.initialize(w, h), pt.lastError()
     assert pt.renderFrames(spp, depth), pt.lastError()
     px, acc = pt.readback()
