@@ -131,7 +131,9 @@ struct State {
     int blocksPerCu = 0;
     bool ldsScene = true;
     int pathMode = 0;             // 0 megakernel, 1 wavefront
-    unsigned wfSlots = 1u << 24;  // wavefront path-state slots per device
+    // wavefront path-state slots per device: 2^27 holds a whole 1080p/64-spp step in flight (one
+    // generation, no regenerate rounds; 8.6 GB of 64-byte records): blob70k 6.8 -> 7.4+ G vs 2^24
+    unsigned wfSlots = 1u << 27;
     hippt::BvhParams bvh;         // applied at the next scene upload
     // host-side timing accumulators
     double traceMs = 0, combineMs = 0;
@@ -1126,7 +1128,7 @@ extern "C" bool hipptSetOption(int key, long long value) {
         s.pathMode = int(value);
         return true;
     case HIPPT_OPT_WAVEFRONT_SLOTS:
-        if (value < 64 || value > (1LL << 26)) return false;
+        if (value < 64 || value > (1LL << 28)) return false;
         s.wfSlots = unsigned(value);
         return true;
     case HIPPT_OPT_BVH_LEAF:
