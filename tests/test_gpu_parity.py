@@ -409,3 +409,54 @@ def test_counting_mode_reports_traversal(pt, mode):
     assert pt.renderFrames(2, 8)
     plain = pt.readback()
     _assert_same(counted[0], counted[1], plain[0], plain[1])
+
+
+@pytest.mark.parametrize("offset", [(0.0, 0.0, 0.0), (2.5e4, -1.0e4, 3.0e4)])
+def test_quantized_tree_far_from_origin(pt, offset):
+    """The 8-bit 4-wide tree read from global memory (LDS scene copy off) stays conservative
+    when the scene and camera sit far from the origin (large |o| in t = q*s*inv + o*inv - o_ray*inv,
+    boxes padded relative to the largest coordinate): bit-exact against the oracle, float
+    nodes and 2-wide tree alike."""
+    import dataclasses
+    base = scenes.blob_scene(64, 34, "blob_small")
+    off = np.asarray(offset, np.float32)
+    sc = dataclasses.replace(base, verts=(base.verts.reshape(-1, 3, 3) + off).reshape(-1, 9).astype(np.float32),
+                             lookfrom=tuple(np.asarray(base.lookfrom, np.float32) + off),
+                             lookat=tuple(np.asarray(base.lookat, np.float32) + off))
+    pt.uploadMesh(sc)
+    w, h = 48, 32
+    ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
+    pt.setOption(hippt.OPT_LDS_SCENE, 0)
+    for width, quant in ((4, 1), (4, 0), (2, -1)):
+        pt.setOption(hippt.OPT_BVH_WIDTH, width)
+        pt.setOption(hippt.OPT_BVH_QUANT, quant)
+        assert pt.initialize(w, h)
+        assert pt.renderFrames(3, 8)
+        got = pt.readback()
+        _assert_same(got[0], got[1], ora[0], ora[1])
+
+
+def test_bench_json_contract():
+    """bench.py prints one JSON line with the driver's keys, the roofline and the CPU baseline
+    objects (a short run: 1 step, sampled CPU baseline)."""
+    import json
+    import os
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--steps", "1", "--warmup", "0",
+                          "--width", "320", "--height", "180", "--cpu-seconds", "1", "--cpu-baseline", "port"],
+                         capture_output=True, text=True, timeout=300, cwd=repo)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [l for l in out.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, out.stdout
+    d = json.loads(lines[0])
+    for k in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+              "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert k in d, k
+    assert d["value"] > 0 and d["n_gpus"] == 1 and d["steps"] == 1
+    r = d["roofline"]
+    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["achieved"] > 0 and r["peak"] == 8000.0
+    assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    cb = d["cpu_baseline"]
+    assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1 and cb["unit"] == "Msamples/s"
