@@ -16,14 +16,16 @@ millions per second; the segment count is the exact count the kernel accumulates
 closest-hit query), so nothing is estimated.
 
 Also reported on rank 0:
-  roofline      the mesh kernel's algorithmic bytes per launch / its mean launch time (HIP
-                events on the library's stream, timed region), against the 8 TB/s HBM peak;
-                bytes per launch from a counted (untimed) pass: 64 B per 2-wide BVH node
-                visit (112 B per 4-wide visit),
-                48 B per triangle test, 32 B per shaded hit, 12 B per sample written
-                (DESIGN.md §Roofline).  traffic = PMC-measured HBM bytes per launch from
-                profiles/ when a matching summary exists, else null; limiters = that
-                summary's VALU issue / texture-addresser busy fractions.
+  roofline      FP32 VALU roofline of the mesh kernel (bound "valu": the path is branchy scalar
+                FP32 over a cache-resident scene, neither HBM- nor MFMA-bound): algorithmic
+                FLOP per launch from a counted (untimed) pass of the same step (20 per child-box
+                slab test, 55 per primitive test, 100 per shading step) / the kernel's mean
+                launch time (HIP events on the library's stream, timed region), vs 157.3
+                TFLOP/s.  From this workload's PMC summary under profiles/ (when present):
+                traffic = HBM bytes per launch, hbm = traffic / launch time vs 8 TB/s,
+                valu_issue / ta_busy, and `limiter` = the busiest of VALU issue, TA and HBM.
+                algorithmic_bytes = the SURVEY.md 8(d) node/primitive/shading bytes (served by
+                LDS/L2/MALL, not HBM).
   cpu_baseline  the reference CPU path tracer (RayTracer.h + Qt-free RenderWorker, built as
                 oracle/_ref/ref_harness) timed on this box's host cores over a bounded row
                 sample of the same workload.
@@ -159,6 +161,46 @@ def load_pmc(args, workload: str):
     return None
 
 
+def make_roofline(args, pmc, traffic, mean_launch_ms, launches, alg_bytes_launch, flops_launch, counted,
+                  alg_gbs) -> dict:
+    """Roofline of the dominant kernel.  This path is branchy scalar FP32 over a cache-resident
+    scene: neither HBM nor MFMA bounds it.  The headline roofline is the FP32 VALU one
+    (algorithmic FLOP per launch from the counted pass / live mean launch time, vs the FP32
+    vector peak); `limiter` names the busiest unit in this workload's PMC profile (VALU issue,
+    the vector-memory texture addresser TA, or HBM), and the HBM fraction is computed from the
+    PMC-measured DRAM bytes, not from the modelled node/primitive bytes (those are served by
+    LDS/L2/MALL; reported as algorithmic_bytes)."""
+    s = mean_launch_ms * 1e-3
+    tflops = flops_launch / s / 1e12 if s > 0 else 0.0
+    r = {"bound": "valu", "achieved": round(tflops, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+         "frac": round(tflops / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
+         "kernel": "mesh_kernel" if args.path_mode == "megakernel" else "wf_extend+wf_shade+wf_generate",
+         "mean_launch_ms": round(mean_launch_ms, 4), "launches_per_step": launches,
+         "flop_per_launch": int(flops_launch),
+         "model": "20 FLOP per child-box slab test (2 per 2-wide, 4 per 4-wide node visit), 55 per primitive "
+                  "test, 100 per shading step",
+         "node_visits_per_step": counted["nodeVisits"], "tri_tests_per_step": counted["triTests"],
+         "algorithmic_bytes": {"per_launch": int(alg_bytes_launch), "achieved_gbs": round(alg_gbs, 2),
+                               "note": "node/primitive/shading bytes of the traversal (SURVEY.md 8d), served "
+                                       "from LDS/L2/MALL; not HBM traffic"}}
+    if pmc:
+        hbm = traffic / s / 1e9 if traffic and s > 0 else None
+        busy = {"valu_issue": pmc.get("valu_issue_busy") or 0.0, "ta": pmc.get("ta_busy") or 0.0,
+                "hbm": (hbm or 0.0) / HBM_PEAK_GBS}
+        r["limiter"] = max(busy, key=busy.get)
+        r["valu_issue"] = {"busy": pmc.get("valu_issue_busy"), "lane_utilization": pmc.get("valu_lane_utilization"),
+                           "note": "fraction of cycles a VALU instruction issues (wave64 = 2 cycles), PMC"}
+        r["ta_busy"] = pmc.get("ta_busy")
+        r["hbm"] = {"achieved": round(hbm, 2) if hbm is not None else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(hbm / HBM_PEAK_GBS, 4) if hbm is not None else None,
+                    "note": "PMC DRAM bytes per launch (FETCH_SIZE + WRITE_SIZE) / live mean launch time"}
+        r["pmc_source"] = pmc.get("source")
+        r["mean_launch_ms_rocprof"] = pmc.get("mean_launch_ms_rocprof")
+    else:
+        r["limiter"] = None
+    return r
+
+
 def main():
     args = parse()
     import torch  # noqa: F401  (torch.distributed for the rank barrier / max-over-ranks)
@@ -283,6 +325,9 @@ def main():
     pmc = load_pmc(args, workload)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
 
+    roofline = make_roofline(args, pmc, traffic, mean_launch_ms, launches, alg_bytes_launch, flops_launch,
+                             counted, achieved)
+
     if rank == 0:
         cpu = cpu_baseline(args, scene) if world == 1 else None
         import zlib
@@ -318,25 +363,7 @@ def main():
                 "chunk": pt._lib.hipptGetOption(hippt.OPT_CHUNK),
                 "image_crc32": zlib.crc32(full.tobytes()) & 0xFFFFFFFF,
             },
-            "roofline": {
-                "bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "kernel": "mesh_kernel" if args.path_mode == "megakernel" else "wf_extend+wf_shade+wf_generate",
-                "mean_launch_ms": round(mean_launch_ms, 4),
-                "launches_per_step": launches,
-                "alg_bytes_per_launch": int(alg_bytes_launch),
-                "node_visits_per_step": counted["nodeVisits"], "tri_tests_per_step": counted["triTests"],
-                # what the profile of this workload says bounds the kernel (not HBM: the scene is
-                # cache-resident): VALU issue and the vector-memory address unit (TA)
-                "limiters": {k: pmc.get(k) for k in ("source", "valu_issue_busy", "valu_lane_utilization",
-                                                     "ta_busy", "hbm_gbs", "mean_launch_ms_rocprof")}
-                if pmc else None,
-                "valu": {"achieved": round(flops_launch / (mean_launch_ms * 1e-3) / 1e12, 3) if mean_launch_ms else 0.0,
-                         "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(flops_launch / (mean_launch_ms * 1e-3) / 1e12 / FP32_PEAK_TFLOPS, 4)
-                         if mean_launch_ms else 0.0,
-                         "model": "20 FLOP/slab test (2 per 2-wide, 4 per 4-wide node visit), 55/triangle test, 100/shading step"},
-            },
+            "roofline": roofline,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

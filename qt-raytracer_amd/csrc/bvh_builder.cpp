@@ -410,28 +410,46 @@ void quantize_bvh4(const Bvh4 &in, std::vector<uint32_t> &out) {
                     hi = std::max(hi, f[8 * a + 4 + i]);
                 }
             if (!(lo <= hi)) lo = hi = 0.0f;  // no used child (never built; kept total)
-            // smallest power-of-two scale with 255 steps covering [lo, hi] (the differences are
-            // exact in double, the scale and the floor/ceil too)
+            // Smallest power-of-two scale s whose grid, with its origin at least one step below
+            // lo, covers [lo, hi] with every plane at least one step outside: a plane is moved
+            // one more step outward when it falls exactly on the grid, so the decoded plane
+            // stays outside the float plane even after the kernel's three roundings of
+            // q*(s*inv) + (o*inv - o_ray*inv) (the float path rounds once).  The differences
+            // are exact in double, the division by s too.
             const double ext = double(hi) - double(lo);
             int e = -100;
             if (ext > 0) {
-                e = int(std::ceil(std::log2(ext / 255.0)));
-                while (std::ldexp(255.0, e) < ext) ++e;
-                while (e > -100 && std::ldexp(255.0, e - 1) >= ext) --e;
+                e = int(std::ceil(std::log2(ext / 253.0)));
+                while (e > -100 && std::ldexp(253.0, e - 1) >= ext) --e;
                 e = std::max(e, -100);
             }
-            origin[a] = lo;
+            uint32_t ql[4], qh[4];
+            float o = lo;
+            for (;; ++e) {
+                const double s = std::ldexp(1.0, e);
+                o = float(double(lo) - s);
+                if (double(o) > double(lo) - s) o = std::nextafter(o, -INFINITY);  // round down
+                bool fits = true;
+                for (int i = 0; i < 4 && fits; ++i) {
+                    ql[i] = 255;  // unused: lo > hi on every axis
+                    qh[i] = 0;
+                    if (!used[i]) continue;
+                    const double xl = (double(f[8 * a + i]) - double(o)) / s;
+                    const double xh = (double(f[8 * a + 4 + i]) - double(o)) / s;
+                    double l = std::floor(xl), h = std::ceil(xh);
+                    if (l == xl) l -= 1.0;
+                    if (h == xh) h += 1.0;
+                    fits = l >= 0.0 && h <= 255.0;
+                    ql[i] = uint32_t(std::max(l, 0.0));
+                    qh[i] = uint32_t(std::min(h, 255.0));
+                }
+                if (fits) break;
+            }
+            origin[a] = o;
             scale[a] = float(std::ldexp(1.0, e));
             for (int i = 0; i < 4; ++i) {
-                uint32_t ql = 255, qh = 0;  // unused: lo > hi on every axis
-                if (used[i]) {
-                    const double l = std::floor((double(f[8 * a + i]) - double(lo)) / scale[a]);
-                    const double h = std::ceil((double(f[8 * a + 4 + i]) - double(lo)) / scale[a]);
-                    ql = uint32_t(std::clamp(l, 0.0, 255.0));
-                    qh = uint32_t(std::clamp(h, 0.0, 255.0));
-                }
-                qlo[a] |= ql << (8 * i);
-                qhi[a] |= qh << (8 * i);
+                qlo[a] |= ql[i] << (8 * i);
+                qhi[a] |= qh[i] << (8 * i);
             }
         }
         std::memcpy(&d[0], origin, 3 * sizeof(float));

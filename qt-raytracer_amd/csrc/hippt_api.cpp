@@ -65,7 +65,8 @@ struct Ctx {
     size_t spillBytes = 0;
     // wavefront path-state pool (allocated on first use)
     void *wfPool = nullptr;
-    unsigned wfSlots = 0;
+    unsigned wfSlots = 0;  // slots allocated
+    unsigned wfWant = 0;   // slots asked for when the pool was allocated (>= wfSlots)
     unsigned *wfCtr = nullptr;
     unsigned *wfHost = nullptr;  // pinned: two snapshots of the ray-queue shard counters
     hipEvent_t wfPoll[2] = {nullptr, nullptr};
@@ -417,17 +418,37 @@ bool ensure_spill(Ctx &c, hippt::MeshParams &p, long long blocks, bool spills, i
 // lag (pinned snapshot + event), so the call returns within ~16 iterations of the end.
 bool run_wavefront(Ctx &c, hippt::MeshParams p, bool cnt, bool spills, int spillCap, const char **err) {
     State &s = S();
-    const unsigned slots = std::max(64u, std::min(s.wfSlots, std::max(64u, p.totalItems)));
+    unsigned slots = std::max(64u, std::min(s.wfSlots, std::max(64u, p.totalItems)));
     unsigned shardCap = 0;
-    const size_t words = hippt::wf_pool_words(slots, &shardCap);
-    if (c.wfSlots != slots || !c.wfPool) {
+    if (c.wfWant != slots || !c.wfPool) {
         HIP_TRY(hipStreamSynchronize(c.stream));
         (void)hipFree(c.wfPool);
         c.wfPool = nullptr;
-        c.wfSlots = 0;
-        HIP_TRY(hipMalloc(&c.wfPool, words * sizeof(uint32_t)));
+        c.wfSlots = c.wfWant = 0;
+        const unsigned want = slots;
+        // Every context owns a pool, and several contexts may share a device (hipptSetDevices
+        // with a repeated id): each takes at most half the device's free memory divided by the
+        // contexts on it, and a failed allocation retries with half the slots.  A smaller pool
+        // only adds regenerate rounds; the image is the same.
+        size_t freeB = 0, totalB = 0;
+        HIP_TRY(hipMemGetInfo(&freeB, &totalB));
+        int sharing = 0;
+        for (const Ctx &o : s.ctxs) sharing += o.device == c.device && !o.wfPool ? 1 : 0;
+        const size_t budget = freeB / 2 / size_t(std::max(1, sharing));
+        while (slots > 64u && hippt::wf_pool_words(slots, &shardCap) * sizeof(uint32_t) > budget) slots >>= 1;
+        for (;;) {
+            const hipError_t e = hipMalloc(&c.wfPool, hippt::wf_pool_words(slots, &shardCap) * sizeof(uint32_t));
+            if (e == hipSuccess) break;
+            (void)hipGetLastError();  // clear the sticky allocation error
+            c.wfPool = nullptr;
+            if (slots <= (1u << 16)) return fail(err, std::string("wavefront pool: ") + hipGetErrorString(e));
+            slots >>= 1;
+        }
         c.wfSlots = slots;
+        c.wfWant = want;
     }
+    slots = c.wfSlots;
+    (void)hippt::wf_pool_words(slots, &shardCap);
     if (!c.wfCtr) HIP_TRY(hipMalloc(&c.wfCtr, hippt::kCtrWords * sizeof(unsigned)));
     hippt::WfParams W{};
     W.mp = p;

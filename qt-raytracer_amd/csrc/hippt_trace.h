@@ -538,12 +538,16 @@ struct SpillArea {
     int cap;        // LDS entries in use at most (the stack content capacity)
 };
 
-__device__ __forceinline__ void spill_bottom(Trav &T, int *my, const SpillArea &S) {
-    const int half = S.cap >> 1, n = T.sp / kMeshBlock;
-    for (int j = 0; j < half; ++j) S.buf[S.base + unsigned(T.ovf + j)] = my[j * kMeshBlock];
-    for (int j = half; j < n; ++j) my[(j - half) * kMeshBlock] = my[j * kMeshBlock];
-    T.sp -= half * kMeshBlock;
-    T.ovf += half;
+// Moves the bottom entries of the LDS stack to the spill area so that `push` more entries fit
+// under the capacity: half the capacity, or more when a small capacity (cap < 6, half < 3)
+// would otherwise let a 4-hit visit (3 pushes) grow the stack past it.
+__device__ __forceinline__ void spill_bottom(Trav &T, int *my, const SpillArea &S, int push) {
+    const int n = T.sp / kMeshBlock;
+    const int k = max(S.cap >> 1, n + push - S.cap);
+    for (int j = 0; j < k; ++j) S.buf[S.base + unsigned(T.ovf + j)] = my[j * kMeshBlock];
+    for (int j = k; j < n; ++j) my[(j - k) * kMeshBlock] = my[j * kMeshBlock];
+    T.sp -= k * kMeshBlock;
+    T.ovf += k;
 }
 
 __device__ __forceinline__ void refill_bottom(Trav &T, int *my, const SpillArea &S) {
@@ -665,7 +669,7 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
         cas(k0, c0, k2, c2);
         cas(k1, c1, k3, c3);
         cas(k1, c1, k2, c2);
-        if (T.sp + (nh - 1) * kMeshBlock > S.cap * kMeshBlock) spill_bottom(T, my, S);
+        if (T.sp + (nh - 1) * kMeshBlock > S.cap * kMeshBlock) spill_bottom(T, my, S, nh - 1);
         // push c[nh-1] .. c1 (c1 on top); unused writes land in the spare slots above
         my[T.sp] = nh == 4 ? c3 : (nh == 3 ? c2 : c1);
         my[T.sp + kMeshBlock] = nh == 4 ? c2 : c1;

@@ -246,6 +246,39 @@ def cornell_mixed() -> Scene:
     return sc
 
 
+def cloud_scene(n: int = 180, seed: int = 7) -> Scene:
+    """Test scene for deep traversal stacks: the Cornell walls around a cloud of n small,
+    randomly oriented triangles filling the box's middle.  Rays cross many overlapping child
+    boxes (4-hit node visits are common), and it still fits the LDS scene copy at n <= 200."""
+    rng = np.random.default_rng(seed)
+    tris, mats = _walls()
+    walls = np.asarray(tris, np.float64).astype(np.float32)
+    c = rng.uniform(120.0, 435.0, size=(n, 1, 3))
+    d = rng.normal(0.0, 18.0, size=(n, 3, 3))
+    cloud = (c + d).reshape(n, 9).astype(np.float32)
+    verts = np.concatenate([walls, cloud], axis=0)
+    tri_mat = np.concatenate([np.asarray(mats, np.int32), np.zeros(n, np.int32)])
+    return Scene(name=f"cloud{n}", verts=np.ascontiguousarray(verts), tri_mat=tri_mat,
+                 albedo=np.asarray([WHITE, GREEN, RED], dtype=np.float32))
+
+
+def voxel_scene(n: int = 6) -> Scene:
+    """Test scene for the 8-bit child boxes: a staircase of unit cubes at integer coordinates
+    (every box plane on a power-of-two quantisation grid, so floor/ceil add no slack) on an
+    integer floor, seen from an integer camera position."""
+    tris = []
+    for i in range(n):
+        for j in range(n):
+            for k in range(max(1, n - i - j)):
+                tris += _box((i, k, j), (i + 1, k + 1, j + 1))
+    tris += _quad((-2, 0, -2), (-2, 0, n + 2), (n + 2, 0, n + 2), (n + 2, 0, -2))
+    verts = np.asarray(tris, np.float64).astype(np.float32)
+    tri_mat = (np.arange(len(tris)) // 12 % 3).astype(np.int32)
+    return Scene(name=f"voxel{n}", verts=verts, tri_mat=tri_mat,
+                 albedo=np.asarray([WHITE, GREEN, RED], dtype=np.float32),
+                 lookfrom=(float(2 * n + 4), float(n + 2), float(2 * n + 6)), lookat=(0.0, 1.0, 0.0), vfov=40.0)
+
+
 SCENES = {"cornell34": cornell34, "blob70k": blob70k, "random_scene": random_scene, "cornell_mixed": cornell_mixed}
 
 

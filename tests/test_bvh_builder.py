@@ -153,12 +153,15 @@ def test_bvh4_collapse_keeps_leaves_and_bounds_subtrees(name):
     assert bound == bvh.stack_bound4 and depth == bvh.depth4
 
 
-@pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene", "cornell_mixed"])
+@pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene", "cornell_mixed", "voxel", "cloud"])
 def test_bvh4_quantized_boxes_contain_float_boxes(name):
     """quantize_bvh4 (hipptBvh4QCopy): every child box decoded exactly (origin + byte * scale, a
-    power-of-two scale) contains the float 4-wide box, each axis uses at most 255 steps of its
-    node's extent, codes are unchanged, and unused slots are inverted (lo 255 > hi 0) boxes."""
-    sc = scenes.get_scene(name)
+    power-of-two scale) contains the float 4-wide box strictly (a plane on the grid moves one
+    step outward, so the kernel's rounding of the decoded plane cannot cull a hit the float box
+    keeps), each axis uses at most 255 steps of its node's extent, codes are unchanged, and
+    unused slots are inverted (lo 255 > hi 0) boxes.  `voxel` puts every plane of integer
+    geometry on the grid."""
+    sc = {"voxel": scenes.voxel_scene, "cloud": scenes.cloud_scene}.get(name, lambda: scenes.get_scene(name))()
     if sc.num_tris == 0:
         pytest.skip("sphere-only scene")
     bvh = hippt.Bvh(sc.verts, extent_hint=800.0)
@@ -179,10 +182,11 @@ def test_bvh4_quantized_boxes_contain_float_boxes(name):
                 continue
             lo = origin[n] + planes[n, :, 0, c] * scale[n]
             hi = origin[n] + planes[n, :, 1, c] * scale[n]
-            assert np.all(lo <= f[n, :, 0, c].astype(np.float64))
-            assert np.all(hi >= f[n, :, 1, c].astype(np.float64))
-        # the scale is the smallest power of two whose 255 steps cover the node's extent
+            assert np.all(lo < f[n, :, 0, c].astype(np.float64))
+            assert np.all(hi > f[n, :, 1, c].astype(np.float64))
+        # the scale is (within a step for the origin's rounding) the smallest power of two whose
+        # 253 steps cover the node's extent (one spare step below and above)
         used = [c for c in range(4) if not (kids[n, c] == -1 and f[n, 0, 0, c] > 1e37)]
         ext = f[n, :, 1, used].max(axis=0).astype(np.float64) - f[n, :, 0, used].min(axis=0).astype(np.float64)
-        assert np.all(255 * scale[n] >= ext)
-        assert np.all((ext == 0) | (255 * scale[n] / 2 < ext))
+        assert np.all(253 * scale[n] >= ext)
+        assert np.all((ext == 0) | (253 * scale[n] / 4 < ext))

@@ -143,6 +143,47 @@ def test_wavefront_equals_megakernel_1080p(pt, slots):
     _assert_same(got[0][0], got[0][1], got[1][0], got[1][1])
 
 
+@pytest.mark.parametrize("slots,w,h,spp", [(None, 1920, 1080, 64), (1 << 28, 3840, 2160, 32)])
+def test_wavefront_large_pools_equal_megakernel(pt, slots, w, h, spp):
+    """The default pool (2^27 slots: the whole 1080p/64 spp bench step in flight, one
+    generation) and the largest one (2^28 slots, 17 GB: a 4K/32 spp call) give the
+    megakernel's image bit for bit (the megakernel is oracle-checked above)."""
+    sc = scenes.blob70k()
+    pt.uploadMesh(sc)
+    lib = hippt.load_library()
+    pt.setOption(hippt.OPT_WAVEFRONT_SLOTS, slots if slots else 1 << 27)
+    got = []
+    for mode in (0, 1):
+        pt.setOption(hippt.OPT_PATH_MODE, mode)
+        assert pt.initialize(w, h)
+        pt.resetStats()
+        assert pt.renderFrames(spp, 8, copy=False), pt.lastError()
+        got.append((pt.readback(), pt.stats()["segments"]))
+    assert lib.hipptGetOption(hippt.OPT_WAVEFRONT_SLOTS) == (slots if slots else 1 << 27)
+    (a, sa), (b, sb) = got
+    assert sa == sb
+    _assert_same(a[0], a[1], b[0], b[1])
+
+
+def test_wavefront_pools_on_a_shared_device(pt):
+    """Three contexts on one device (hipptSetDevices([0, 0, 0])), wavefront mode with the
+    default 2^27-slot request: each context's pool is sized to its share of the device's free
+    memory (or retried smaller), and the image equals the one-context render."""
+    sc = scenes.blob70k()
+    pt.uploadMesh(sc)
+    pt.setOption(hippt.OPT_PATH_MODE, 1)
+    pt.setOption(hippt.OPT_WAVEFRONT_SLOTS, 1 << 27)
+    w, h = 960, 540
+    assert pt.initialize(w, h)
+    assert pt.renderFrames(16, 8)
+    one = pt.readback()
+    pt.setDevices([0, 0, 0])
+    assert pt.initialize(w, h)
+    assert pt.renderFrames(16, 8), pt.lastError()
+    three = pt.readback()
+    _assert_same(one[0], one[1], three[0], three[1])
+
+
 def _general_scene(name, golden_dir):
     if name == "ref_random_scene":
         return scenes.load_scene_file(os.path.join(golden_dir, "ref_random_scene.scene"), name)
@@ -269,6 +310,44 @@ def test_bvh_width_and_stack_spill_do_not_change_results(pt, name):
             assert pt.renderFrames(3, 8)
             got = pt.readback()
             _assert_same(got[0], got[1], ora[0], ora[1])
+
+
+@pytest.mark.parametrize("mode", [0, 1])
+def test_small_stack_cap_on_deep_lds_scene(pt, mode):
+    """LDS-resident scene with a deep 4-wide tree (cloud180: stack bound 16) traversed with the
+    smallest LDS stack caps (4 and 5: half the cap is below the 3 pushes of a 4-hit visit, so
+    the spill must move more than half) and the default: the spill never writes past the lane's
+    LDS stack (which would corrupt the block's LDS scene copy); bit-exact against the oracle,
+    megakernel and wavefront."""
+    sc = scenes.cloud_scene(180)
+    pt.uploadMesh(sc)
+    pt.setOption(hippt.OPT_PATH_MODE, mode)
+    w, h = 64, 48
+    ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
+    for cap in (4, 5, 6, 0):
+        pt.setOption(hippt.OPT_STACK_CAP, cap)
+        assert pt.initialize(w, h)
+        assert pt.renderFrames(3, 8)
+        got = pt.readback()
+        _assert_same(got[0], got[1], ora[0], ora[1])
+
+
+def test_quantized_tree_grid_aligned_geometry(pt):
+    """Integer-coordinate cubes (every child-box plane on its node's power-of-two grid) read
+    from global memory with 8-bit child boxes: bit-exact against the oracle, as the float
+    4-wide and the 2-wide trees."""
+    sc = scenes.voxel_scene(6)
+    pt.uploadMesh(sc)
+    pt.setOption(hippt.OPT_LDS_SCENE, 0)
+    w, h = 64, 48
+    ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
+    for width, quant in ((4, 1), (4, 0), (2, -1)):
+        pt.setOption(hippt.OPT_BVH_WIDTH, width)
+        pt.setOption(hippt.OPT_BVH_QUANT, quant)
+        assert pt.initialize(w, h)
+        assert pt.renderFrames(3, 8)
+        got = pt.readback()
+        _assert_same(got[0], got[1], ora[0], ora[1])
 
 
 def test_mesh_batches_and_frame_splits_are_bit_identical(pt):
@@ -456,7 +535,8 @@ def test_bench_json_contract():
         assert k in d, k
     assert d["value"] > 0 and d["n_gpus"] == 1 and d["steps"] == 1
     r = d["roofline"]
-    assert r["bound"] == "hbm" and r["unit"] == "GB/s" and r["achieved"] > 0 and r["peak"] == 8000.0
+    assert r["bound"] == "valu" and r["unit"] == "TFLOP/s" and r["achieved"] > 0 and r["peak"] == 157.3
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
+    assert r["algorithmic_bytes"]["per_launch"] > 0
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1 and cb["unit"] == "Msamples/s"
