@@ -36,7 +36,7 @@ namespace {
 
 using hippt::CameraF;
 
-constexpr int kStatWords = 32;  // [0..3] hipptStats counters, [4..19] phase profile
+constexpr int kStatWords = 32;  // [0..3] hipptStats counters, [4..19] phase profile, [20..24] hit-children histogram
 
 // 4-wide traversal: LDS stack content capacity for scenes outside LDS (19 + 3 spare entries =
 // 22 KB per 256-lane block: 7 blocks per CU in 160 KB).
@@ -390,9 +390,10 @@ bool init_locked(int width, int height, const char **err) {
     return false;
 }
 
-long long occupancy_key(int version, int stackDepth, bool lds, bool full, bool wide = false, bool quant = false) {
-    return ((long long)version << 10) | (stackDepth << 4) | (quant ? 8 : 0) | (wide ? 4 : 0) | (lds ? 2 : 0) |
-           (full ? 1 : 0);
+long long occupancy_key(int version, int stackDepth, bool lds, bool full, bool wide = false, bool quant = false,
+                        bool spills = true) {
+    return ((long long)version << 11) | ((long long)stackDepth << 5) | (spills ? 16 : 0) | (quant ? 8 : 0) |
+           (wide ? 4 : 0) | (lds ? 2 : 0) | (full ? 1 : 0);
 }
 
 // 4-wide traversal of a tree whose stack bound exceeds the LDS capacity: a per-lane spill
@@ -594,13 +595,13 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 // (random_scene, general kernel: 20.9 -> 18.5 G).
                 const bool quant = wide && !ldsScene && (s.bvhQuant == 1 || (s.bvhQuant == -1 && !s.scene.full));
                 const long long occKey =
-                    occupancy_key(s.scene.version, stackDepth, ldsScene, s.scene.full, wide, quant);
+                    occupancy_key(s.scene.version, stackDepth, ldsScene, s.scene.full, wide, quant, spills);
                 if (c.occKey != occKey) {
                     const int ln = ldsScene ? numNodes : 0, lt = ldsScene ? numTris : 0;
                     c.meshBlocksPerCu[0] =
-                        hippt::mesh_blocks_per_cu(false, s.scene.full, wide, quant, stackDepth, ln, lt);
+                        hippt::mesh_blocks_per_cu(false, s.scene.full, wide, quant, stackDepth, ln, lt, spills);
                     c.meshBlocksPerCu[1] =
-                        hippt::mesh_blocks_per_cu(true, s.scene.full, wide, quant, stackDepth, ln, lt);
+                        hippt::mesh_blocks_per_cu(true, s.scene.full, wide, quant, stackDepth, ln, lt, spills);
                     c.occKey = occKey;
                 }
                 int bpc = s.blocksPerCu > 0 ? s.blocksPerCu : c.meshBlocksPerCu[cnt ? 1 : 0];

@@ -80,7 +80,7 @@ hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hip
 hipError_t launch_combine(const CombineParams &p, hipStream_t s);
 // Resident mesh-kernel blocks per CU for a given LDS stack depth and LDS scene size.
 int mesh_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,
-                       int ldsTris);
+                       int ldsTris, bool spill);
 size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide);
 size_t mesh_lds_scene_limit();
 constexpr int kMeshBlock = 256;

@@ -187,7 +187,7 @@ __device__ unsigned long long g_timeline[65536 * 6];
 #ifndef HIPPT_WIDE_WAVES_PER_EU
 #define HIPPT_WIDE_WAVES_PER_EU 7
 #endif
-template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE, bool QUANT>
+template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE, bool QUANT, bool SPILL = true>
 __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_EU : HIPPT_MESH_WAVES_PER_EU) HIPPT_SGPR_ATTR void mesh_kernel(MeshParams P) {
     static_assert(!QUANT || (WIDE && !LDS_SCENE), "quantized nodes: 4-wide global-memory traversal only");
 #ifdef HIPPT_DEBUG_TIMELINE
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     // for the wave sum
     unsigned segs = 0, samples = 0;
     unsigned long long nvis = 0, ntest = 0;
-    unsigned pc[16] = {0};
+    unsigned pc[kProfSlots] = {0};
 
     for (;;) {
         prof<STATS>(pc, 0);
@@ -276,7 +276,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         do {
             prof<STATS>(pc, 2);
             if (WIDE)
-                traverse_round_wide<nodeF4, STATS, FULL, QUANT>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit,
+                traverse_round_wide<nodeF4, STATS, FULL, QUANT, SPILL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit,
                                                                 P.nodeExit, S);
             else
                 traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
@@ -330,7 +330,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     }
     if (STATS) {
 #pragma unroll
-        for (int k = 0; k < 16; ++k) {
+        for (int k = 0; k < kProfSlots; ++k) {
             const unsigned long long v = wave_sum(pc[k]);
             if (__lane_id() == 0) atomicAdd(&P.stats[4 + k], v);
         }
@@ -391,15 +391,23 @@ static constexpr int kMaxResidentBlocks = 800 / (HIPPT_NUM_SGPR + 16) < 8 ? 800 
 
 using MeshFn = void (*)(MeshParams);
 // node formats: 2-wide, 4-wide float, 4-wide quantized (global memory only)
-template <bool STATS, bool FULL>
-static MeshFn mesh_fn_fmt(bool lds, bool wide, bool quant) {
-    if (lds) return wide ? mesh_kernel<STATS, true, FULL, true, false> : mesh_kernel<STATS, true, FULL, false, false>;
-    if (!wide) return mesh_kernel<STATS, false, FULL, false, false>;
-    return quant ? mesh_kernel<STATS, false, FULL, true, true> : mesh_kernel<STATS, false, FULL, true, false>;
+// 4-wide trees whose stack bound fits the LDS capacity run a variant without the spill/refill
+// code (timed builds; the counting builds keep one variant, the results are the same)
+template <bool STATS, bool FULL, bool SPILL>
+static MeshFn mesh_fn_wide(bool lds, bool quant) {
+    if (lds) return mesh_kernel<STATS, true, FULL, true, false, SPILL>;
+    return quant ? mesh_kernel<STATS, false, FULL, true, true, SPILL> : mesh_kernel<STATS, false, FULL, true, false, SPILL>;
 }
-static MeshFn mesh_fn(bool count, bool lds, bool full, bool wide, bool quant) {
-    if (count) return full ? mesh_fn_fmt<true, true>(lds, wide, quant) : mesh_fn_fmt<true, false>(lds, wide, quant);
-    return full ? mesh_fn_fmt<false, true>(lds, wide, quant) : mesh_fn_fmt<false, false>(lds, wide, quant);
+template <bool STATS, bool FULL>
+static MeshFn mesh_fn_fmt(bool lds, bool wide, bool quant, bool spill) {
+    if (!wide) return lds ? mesh_kernel<STATS, true, FULL, false, false> : mesh_kernel<STATS, false, FULL, false, false>;
+    if (STATS || spill) return mesh_fn_wide<STATS, FULL, true>(lds, quant);
+    return mesh_fn_wide<STATS, FULL, false>(lds, quant);
+}
+static MeshFn mesh_fn(bool count, bool lds, bool full, bool wide, bool quant, bool spill) {
+    if (count)
+        return full ? mesh_fn_fmt<true, true>(lds, wide, quant, spill) : mesh_fn_fmt<true, false>(lds, wide, quant, spill);
+    return full ? mesh_fn_fmt<false, true>(lds, wide, quant, spill) : mesh_fn_fmt<false, false>(lds, wide, quant, spill);
 }
 
 hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hipStream_t s) {
@@ -407,7 +415,8 @@ hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hip
     if (p.wide && (p.stackCap < 1 || p.stackCap + 2 > p.stackDepth)) return hipErrorInvalidValue;
     const bool lds = p.ldsScene != 0;
     const size_t bytes = mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0, p.wide != 0);
-    hipLaunchKernelGGL(mesh_fn(countTraversal, lds, p.full != 0, p.wide != 0, p.wide == 2 && !lds), dim3(blocks),
+    hipLaunchKernelGGL(mesh_fn(countTraversal, lds, p.full != 0, p.wide != 0, p.wide == 2 && !lds, p.spill != nullptr),
+                       dim3(blocks),
                        dim3(kMeshBlock), bytes, s, p);
     return hipGetLastError();
 }
@@ -421,12 +430,12 @@ hipError_t launch_combine(const CombineParams &p, hipStream_t s) {
 }
 
 int mesh_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,
-                       int ldsTris) {
+                       int ldsTris, bool spill) {
     int n = 0;
     const bool lds = ldsNodes > 0;
     const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, wide);
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &n, mesh_fn(countTraversal, lds, full, wide, quant && wide && !lds), kMeshBlock, bytes);
+        &n, mesh_fn(countTraversal, lds, full, wide, quant && wide && !lds, spill), kMeshBlock, bytes);
     if (e != hipSuccess || n <= 0) n = 1;
     // the query ignores the trap handler's SGPRs (kMaxResidentBlocks): a larger persistent grid
     // leaves blocks waiting for a slot until others finish

@@ -183,7 +183,10 @@ __device__ __forceinline__ void wave_append(bool req, unsigned value, unsigned *
 // Phase profiling (STATS builds): pc[2k] counts wave-level passes of phase k (by the first
 // active lane), pc[2k+1] lane-level passes; SIMD efficiency = lanes / (64 * waves).  Phases:
 // 0 outer iteration, 1 camera ray, 2 traversal round, 3 interior node loop, 4 leaf loop,
-// 5 primitive test, 6 shading, 7 unit-sphere rejection loop.
+// 5 primitive test, 6 shading, 7 unit-sphere rejection loop.  pc[kNhHist + h] (4-wide trees)
+// counts node visits with h = 0..4 hit children; pc[kNhHist + 5] those with none hit only
+// because of the closest hit found since the node was pushed (float 4-wide nodes).
+constexpr int kProfPhases = 8, kNhHist = 2 * kProfPhases, kProfSlots = kNhHist + 6;
 template <bool STATS>
 __device__ __forceinline__ void prof(unsigned *pc, int k) {
     if (STATS) {
@@ -413,11 +416,9 @@ __device__ __forceinline__ void begin(Trav &T) {
 
 // Primitive i (leaf order) against the ray: closest hit = min (t, primitive id).
 template <bool STATS, bool FULL>
-__device__ __forceinline__ void test_prim(Trav &T, const Ray &r, const float4 *tris, int i, unsigned long long &ntest,
-                                          unsigned *pc) {
+__device__ __forceinline__ void test_prim_data(Trav &T, const Ray &r, float4 A, float4 B, float4 Cc, int i,
+                                               unsigned long long &ntest, unsigned *pc) {
     const float tmin = 0.001f;
-    const float4 *tp = tris + 3 * i;
-    const float4 A = tp[0], B = tp[1], Cc = tp[2];
     prof<STATS>(pc, 5);
     if (STATS) ++ntest;
     if (FULL && __float_as_int(Cc.z) != 0) {
@@ -454,6 +455,13 @@ __device__ __forceinline__ void test_prim(Trav &T, const Ray &r, const float4 *t
             T.bestO = orig;
         }
     }
+}
+
+template <bool STATS, bool FULL>
+__device__ __forceinline__ void test_prim(Trav &T, const Ray &r, const float4 *tris, int i, unsigned long long &ntest,
+                                          unsigned *pc) {
+    const float4 *tp = tris + 3 * i;
+    test_prim_data<STATS, FULL>(T, r, tp[0], tp[1], tp[2], i, ntest, pc);
 }
 
 // One leaf-loop iteration for this lane: the primitives of leaf T.leaf, then the next leaf if it
@@ -557,8 +565,9 @@ __device__ __forceinline__ void refill_bottom(Trav &T, int *my, const SpillArea 
     T.sp = n * kMeshBlock;
 }
 
+template <bool SPILL = true>
 __device__ __forceinline__ int pop_wide(Trav &T, int *my, const SpillArea &S) {
-    if (T.sp == 0 && T.ovf != 0) refill_bottom(T, my, S);
+    if (SPILL && T.sp == 0 && T.ovf != 0) refill_bottom(T, my, S);
     if (T.sp == 0) return kDone;
     T.sp -= kMeshBlock;
     return my[T.sp];
@@ -612,8 +621,9 @@ __device__ __forceinline__ void cas(unsigned &ka, int &ca, unsigned &kb, int &cb
 }
 
 // traverse_round over the 4-wide tree: a node visit tests its four child boxes, descends into
-// the nearest hit child and pushes the other hit children far to near.
-template <int NODE_F4, bool STATS, bool FULL, bool QUANT = false>
+// the nearest hit child and pushes the other hit children far to near.  SPILL=false: the tree's
+// stack bound fits the LDS capacity (no spill/refill code in the loop).
+template <int NODE_F4, bool STATS, bool FULL, bool QUANT = false, bool SPILL = true>
 __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *my, const float4 *nodes,
                                                     const float4 *tris, unsigned long long &nvis,
                                                     unsigned long long &ntest, unsigned *pc, unsigned leafExit,
@@ -639,6 +649,13 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
             k1 = child_key(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, r, tmin, T.bestT);
             k2 = child_key(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z, r, tmin, T.bestT);
             k3 = child_key(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w, r, tmin, T.bestT);
+            if (STATS && (k0 & k1 & k2 & k3) == 0xffffffffu) {
+                const unsigned u = child_key(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, r, tmin, INFINITY) &
+                                   child_key(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, r, tmin, INFINITY) &
+                                   child_key(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z, r, tmin, INFINITY) &
+                                   child_key(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w, r, tmin, INFINITY);
+                if (u != 0xffffffffu) ++pc[kNhHist + 5];
+            }
         } else {
             // 64-byte node (bvh_builder.h quantize_bvh4): 4 loads instead of 7.  Plane q of axis
             // a enters the slab test as t = q*(s*inv) + (o*inv - o_ray*inv).
@@ -662,6 +679,7 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
         if (STATS) ++nvis;
         // hit children: a miss key is all ones (bit 31), a hit key a positive float's bits
         const int nh = 4 - int((k0 >> 31) + (k1 >> 31) + (k2 >> 31) + (k3 >> 31));
+        if (STATS) ++pc[kNhHist + nh];
         // sorting network (0,1)(2,3)(0,2)(1,3)(1,2), codes carried along: c0 nearest
         int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
         cas(k0, c0, k1, c1);
@@ -669,23 +687,23 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
         cas(k0, c0, k2, c2);
         cas(k1, c1, k3, c3);
         cas(k1, c1, k2, c2);
-        if (T.sp + (nh - 1) * kMeshBlock > S.cap * kMeshBlock) spill_bottom(T, my, S, nh - 1);
+        if (SPILL && T.sp + (nh - 1) * kMeshBlock > S.cap * kMeshBlock) spill_bottom(T, my, S, nh - 1);
         // push c[nh-1] .. c1 (c1 on top); unused writes land in the spare slots above
         my[T.sp] = nh == 4 ? c3 : (nh == 3 ? c2 : c1);
         my[T.sp + kMeshBlock] = nh == 4 ? c2 : c1;
         my[T.sp + 2 * kMeshBlock] = c1;
         T.sp += nh > 1 ? (nh - 1) * kMeshBlock : 0;
-        T.cur = nh > 0 ? c0 : pop_wide(T, my, S);
+        T.cur = nh > 0 ? c0 : pop_wide<SPILL>(T, my, S);
         // postpone the first leaf reached and keep descending
         if (T.cur < 0 && T.cur != kDone && T.leaf == 0) {
             T.leaf = T.cur;
-            T.cur = pop_wide(T, my, S);
+            T.cur = pop_wide<SPILL>(T, my, S);
         }
         if (__popcll(__ballot(T.leaf == 0 && T.cur >= 0)) <= leafExit) break;
     }
     while (T.leaf != 0) {
         prof<STATS>(pc, 4);
-        leaf_step<STATS, FULL>(T, r, tris, ntest, pc, [&] { return pop_wide(T, my, S); });
+        leaf_step<STATS, FULL>(T, r, tris, ntest, pc, [&] { return pop_wide<SPILL>(T, my, S); });
         if (nodeExit && __popcll(__ballot(T.leaf != 0)) <= nodeExit) break;
     }
 }

@@ -150,7 +150,7 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
     T.bestI = -1;
     T.bestO = 0x7fffffff;
     unsigned long long nvis = 0, ntest = 0;
-    unsigned pc[16] = {};  // phase profile slots (not reported by the wavefront path)
+    unsigned pc[kProfSlots] = {};  // phase profile slots (not reported by the wavefront path)
     for (;;) {
         while (left && __ballot(need)) {
             const unsigned qi =

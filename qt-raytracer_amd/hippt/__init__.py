@@ -429,6 +429,10 @@ class PathTracer:
         for k, name in enumerate(self.PHASES):
             w, l = v[4 + 2 * k], v[5 + 2 * k]
             out[name] = {"wave": w, "lane": l, "simd_eff": round(l / (64 * w), 4) if w else None}
+        # 4-wide node visits by number of hit children (0..4)
+        out["hit_children"] = v[20:25]
+        # of the visits with none hit: those with a child box hit before the closest-hit cut
+        out["culled_by_best_t"] = v[25]
         return out
 
     def resetStats(self) -> None:  # noqa: N802

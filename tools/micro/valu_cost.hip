@@ -52,7 +52,15 @@
     X(k_sqrt, "v_sqrt_f32 %0, %0")                                    \
     X(k_perm, "v_perm_b32 %0, %0, %1, %2")                            \
     X(k_xad, "v_xad_u32 %0, %0, %1, %2")                              \
-    X(k_dpp, "v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf")
+    X(k_dpp, "v_mov_b32_dpp %0, %1 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf") \
+    X(k_fma_mix, "v_fma_mix_f32 %0, %2, %1, %0 op_sel_hi:[1,0,0]")   \
+    X(k_fma_mix_hi, "v_fma_mix_f32 %0, %2, %1, %0 op_sel:[1,0,0] op_sel_hi:[1,0,0]") \
+    X(k_cvt_f16, "v_cvt_f32_f16 %0, %0")                              \
+    X(k_xor_sdwa, "v_xor_b32_sdwa %0, %0, %0 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:WORD_1 src1_sel:DWORD") \
+    X(k_max_f16, "v_max_f16 %0, %0, %1")                              \
+    X(k_pk_max_f16, "v_pk_max_f16 %0, %0, %1")                        \
+    X(k_alignbit, "v_alignbit_b32 %0, %0, %0, 15")                    \
+    X(k_mul_hi, "v_mul_hi_u32 %0, %0, %1")                           
 
 #define DEF(NAME, S) KERNEL(NAME, S)
 LIST(DEF)

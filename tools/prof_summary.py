@@ -80,7 +80,9 @@ def main():
         "mean_launch_ms_bench_events": bench["roofline"]["mean_launch_ms"],
         "hbm_bytes_per_launch": int(hbm), "fetch_bytes_raw_per_launch": int(fetch_raw),
         "write_bytes_per_launch": int(write),
-        "alg_bytes_per_launch": bench["roofline"]["alg_bytes_per_launch"],
+        "alg_bytes_per_launch": bench["roofline"].get("alg_bytes_per_launch")
+        or bench["roofline"]["algorithmic_bytes"]["per_launch"],
+        "flop_per_launch": bench["roofline"].get("flop_per_launch"),
         "hbm_gbs": round(hbm / (mean_ms * 1e-3) / 1e9, 2),
         "waves_per_launch": c.get("SQ_WAVES"), "valu_insts_per_launch": c.get("SQ_INSTS_VALU"),
         "salu_insts_per_launch": c.get("SQ_INSTS_SALU"), "vmem_rd_insts_per_launch": c.get("SQ_INSTS_VMEM_RD"),
