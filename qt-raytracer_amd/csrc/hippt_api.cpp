@@ -817,6 +817,20 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
     hippt::quantize_bvh4(bvh4, q);
     sc.nodes4q.assign(q.size() / 4, float4{});
     std::memcpy(sc.nodes4q.data(), q.data(), q.size() * sizeof(uint32_t));
+    if (bvh4.nodes.size() / hippt::kNode4Words >= (1u << 24)) return fail(err, "4-wide BVH too large (2^24 nodes)");
+    // device layouts of the 4-wide trees: an interior child's code is its node's BYTE offset (the
+    // kernels address a node without a multiply; leaf codes and the root, 0, are unchanged)
+    auto byte_codes = [](std::vector<float4> &v, int nodeWords, int codeWord, int stride) {
+        auto *w = reinterpret_cast<int32_t *>(v.data());
+        const size_t n = v.size() * 4 / size_t(nodeWords);
+        for (size_t k = 0; k < n; ++k)
+            for (int i = 0; i < 4; ++i) {
+                int32_t &c = w[k * size_t(nodeWords) + size_t(codeWord + i)];
+                if (c >= 0) c *= stride;
+            }
+    };
+    byte_codes(sc.nodes4, hippt::kNode4Words, 24, hippt::kNode4Words * 4);
+    byte_codes(sc.nodes4q, hippt::kNode4QWords, 12, hippt::kNode4QWords * 4);
     sc.levels4 = bvh4.levels;
     sc.stackBound4 = bvh4.stackBound;
     sc.tris.assign(size_t(numPrims) * 3, float4{});

@@ -84,5 +84,11 @@ int mesh_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, in
 size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide);
 size_t mesh_lds_scene_limit();
 constexpr int kMeshBlock = 256;
+// LDS-resident scene copies: 2-wide nodes at an 80-byte stride, 4-wide nodes in the 128-byte
+// global layout (the octant row addressing by or/xor needs 128-byte alignment; a 144- or
+// 160-byte stride cut the LDS bank conflicts of node rows by 40% but not the kernel time, and
+// the add-based addressing it needs costs registers: spills in the general kernels).
+constexpr int kLdsNodeF4 = 5;
+constexpr int kLdsNode4F4 = 8;
 
 }  // namespace hippt

@@ -160,12 +160,8 @@ __global__ __launch_bounds__(256) void sphere4_kernel(Sphere4Params P) {
 #define HIPPT_MESH_WAVES_PER_EU 1
 #endif
 
-// LDS-resident scene (small scenes): nodes at an 80-byte stride (20 dwords: 16 nodes start on
-// 16 distinct 4-bank groups, so ds_read_b128 of different nodes in a lane group do not
-// conflict), primitives at 48 bytes (12 dwords, likewise), shading records at 16 bytes.
-constexpr int kLdsNodeF4 = 5;
-// 4-wide nodes in LDS: the global 128-byte layout (row addresses by or/xor of the octant offsets).
-constexpr int kLdsNode4F4 = 8;
+// LDS-resident scene (small scenes): node strides kLdsNodeF4 / kLdsNode4F4 (hippt_device.h),
+// primitives at 48 bytes (12 dwords: conflict-free likewise), shading records at 16 bytes.
 
 #ifdef HIPPT_DEBUG_TIMELINE
 // per wave: [0] start, [1] first drained fetch, [2] end (s_memrealtime, 100 MHz), [3] items,

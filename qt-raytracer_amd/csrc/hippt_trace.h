@@ -526,7 +526,7 @@ __device__ __forceinline__ void traverse_round(Trav &T, const Ray &r, int *my, c
             T.cur = T.sp > 0 ? my[T.sp -= kMeshBlock] : kDone;
         }
         // leave for the leaf loop once at most leafExit lanes still search for their first leaf
-        if (__popcll(__ballot(T.leaf == 0 && T.cur >= 0)) <= leafExit) break;
+        if (__popcll(__ballot((T.leaf | T.cur) >= 0)) <= leafExit) break;
     }
     while (T.leaf != 0) {
         prof<STATS>(pc, 4);
@@ -573,6 +573,15 @@ __device__ __forceinline__ int pop_wide(Trav &T, int *my, const SpillArea &S) {
     return my[T.sp];
 }
 
+// min(a, b) as one v_min_f32: fminf() of the loop-carried bestT makes the compiler quieten a
+// possible signaling NaN first (a v_max_f32 b, b per node visit); the box test has no NaN
+// (finite padded boxes, clamped reciprocals), and v_min_f32 of non-NaN inputs is fminf.
+__device__ __forceinline__ float fmin_raw(float a, float b) {
+    float d;
+    asm("v_min_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+
 // Sort key of a child box from its near and far planes on each axis (the ray's direction signs
 // choose them, see traverse_round_wide): entry distance bits (>= tmin > 0, so ordered as
 // unsigned); a miss sorts last.  Two min/max per bound instead of five: the planes need no
@@ -583,7 +592,7 @@ __device__ __forceinline__ unsigned child_key(float nx, float fx, float ny, floa
     const float ay = fmaf(ny, r.iy, -r.oiy), by = fmaf(fy, r.iy, -r.oiy);
     const float az = fmaf(nz, r.iz, -r.oiz), bz = fmaf(fz, r.iz, -r.oiz);
     const float n = fmaxf(fmaxf(ax, ay), fmaxf(az, tmin));
-    const float f = fminf(fminf(bx, by), fminf(bz, bestT));
+    const float f = fminf(fminf(bx, by), fmin_raw(bz, bestT));
     return n <= f ? __float_as_uint(n) : 0xffffffffu;
 }
 
@@ -597,7 +606,7 @@ __device__ __forceinline__ unsigned child_key_q(unsigned nxw, unsigned fxw, unsi
     const float tny = fmaf(float((nyw >> (8 * I)) & 0xffu), by, ay), tfy = fmaf(float((fyw >> (8 * I)) & 0xffu), by, ay);
     const float tnz = fmaf(float((nzw >> (8 * I)) & 0xffu), bz, az), tfz = fmaf(float((fzw >> (8 * I)) & 0xffu), bz, az);
     const float n = fmaxf(fmaxf(tnx, tny), fmaxf(tnz, tmin));
-    const float f = fminf(fminf(tfx, tfy), fminf(tfz, bestT));
+    const float f = fminf(fminf(tfx, tfy), fmin_raw(tfz, bestT));
     return n <= f ? __float_as_uint(n) : 0xffffffffu;
 }
 
@@ -634,13 +643,15 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
     while (T.cur >= 0) {
         prof<STATS>(pc, 3);
         // rows lo.x hi.x lo.y hi.y lo.z hi.z: read as near/far rows of this ray's octant (32-bit
-        // byte offsets from the uniform base: base-register + offset-register loads)
-        const unsigned nb = __umul24(unsigned(T.cur), unsigned(NODE_F4 * 16));
+        // byte offsets from the uniform base: base-register + offset-register loads).  NODE_F4
+        // (the node stride) is implied by the codes: the device trees store byte offsets.
+        const unsigned nb = unsigned(T.cur);  // interior codes are node byte offsets
         unsigned k0, k1, k2, k3;
         int4 ch;
         if (!QUANT) {
-            // 128-byte float nodes (NODE_F4 == 8, LDS and global): nb's low 7 bits are zero
-            const unsigned ax = nb | sx, ay = nb | sy, az = nb | sz;  // near rows; far = near ^ 16
+            // 128-byte float nodes (LDS and global): nb's low 7 bits are zero, so the octant's
+            // near row is nb | s and the far row its ^ 16
+            const unsigned ax = nb | sx, ay = nb | sy, az = nb | sz;
             const float4 nx = ld4(nodes, ax), fx = ld4(nodes, ax ^ 16u);
             const float4 ny = ld4(nodes, ay), fy = ld4(nodes, ay ^ 16u);
             const float4 nz = ld4(nodes, az), fz = ld4(nodes, az ^ 16u);
@@ -699,7 +710,7 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
             T.leaf = T.cur;
             T.cur = pop_wide<SPILL>(T, my, S);
         }
-        if (__popcll(__ballot(T.leaf == 0 && T.cur >= 0)) <= leafExit) break;
+        if (__popcll(__ballot((T.leaf | T.cur) >= 0)) <= leafExit) break;
     }
     while (T.leaf != 0) {
         prof<STATS>(pc, 4);

@@ -117,21 +117,22 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
         }
     }
     const float4 *nodes = P.nodes, *tris = P.tris;
-    constexpr int ldsNodeF4 = WIDE ? 8 : 5;  // mesh_lds_bytes layout
+    constexpr int ldsNodeF4 = WIDE ? kLdsNode4F4 : kLdsNodeF4;  // mesh_lds_bytes layout
     if (LDS_SCENE) {
         float4 *sNodes = reinterpret_cast<float4 *>(stk + (P.stackDepth + 1) * kMeshBlock);
         float4 *sTris = sNodes + P.numNodes * ldsNodeF4;
         if (WIDE) {
-            for (int i = threadIdx.x; i < P.numNodes * 8; i += kMeshBlock) sNodes[i] = P.nodes[i];
+            for (int i = threadIdx.x; i < P.numNodes * kLdsNode4F4; i += kMeshBlock) sNodes[i] = P.nodes[i];
         } else {
-            for (int i = threadIdx.x; i < P.numNodes * 4; i += kMeshBlock) sNodes[(i >> 2) * 5 + (i & 3)] = P.nodes[i];
+            for (int i = threadIdx.x; i < P.numNodes * 4; i += kMeshBlock)
+                sNodes[(i >> 2) * kLdsNodeF4 + (i & 3)] = P.nodes[i];
         }
         for (int i = threadIdx.x; i < P.numTris * 3; i += kMeshBlock) sTris[i] = P.tris[i];
         __syncthreads();
         nodes = sNodes;
         tris = sTris;
     }
-    constexpr int nodeF4 = WIDE ? (QUANT ? 4 : 8) : (LDS_SCENE ? 5 : 4);
+    constexpr int nodeF4 = WIDE ? (QUANT ? 4 : (LDS_SCENE ? kLdsNode4F4 : 8)) : (LDS_SCENE ? kLdsNodeF4 : 4);
     const SpillArea S{P.spill, (blockIdx.x * unsigned(kMeshBlock) + threadIdx.x) * unsigned(P.spillCap), P.stackCap};
     const unsigned *queue = cur ? W.extQ1 : W.extQ0;
     // each wave drains its block's home shard first, then the others in turn (one fetch
