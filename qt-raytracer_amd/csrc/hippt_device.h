@@ -75,6 +75,15 @@ struct CombineParams {
 enum { kLambertian = 0, kMetal = 1, kDielectric = 2 };
 constexpr int kShadeSphere = 1 << 30;
 
+// The LDS-scene kernels read the node copy at LDS address 0 (trace::lds_ld4): true when the
+// kernel has no static LDS, so that its dynamic LDS starts at address 0.
+inline hipError_t check_lds_at_zero(const void *kernel) {
+    hipFuncAttributes a{};
+    const hipError_t e = hipFuncGetAttributes(&a, kernel);
+    if (e != hipSuccess) return e;
+    return a.sharedSizeBytes == 0 ? hipSuccess : hipErrorInvalidDeviceFunction;
+}
+
 hipError_t launch_sphere4(const Sphere4Params &p, hipStream_t s);
 hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hipStream_t s);
 hipError_t launch_combine(const CombineParams &p, hipStream_t s);

@@ -198,14 +198,17 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     // Per-lane traversal stack, P.stackDepth (= BVH interior levels) entries per lane, sized
     // at launch so shallow BVHs do not cap occupancy.  Entry k of lane t at stk[k*256 + t]:
     // a wave's lanes hit 64 consecutive dwords, conflict-free for any mix of depths.
-    extern __shared__ int stk[];
+    // LDS-resident scenes put the node copy at LDS address 0 (node rows are then addressed by
+    // their byte offset alone: no base add per row read), then the stack, primitives, shading.
+    extern __shared__ int lds[];
+    constexpr int ldsNodeF4 = WIDE ? kLdsNode4F4 : kLdsNodeF4;
+    int *const stk = LDS_SCENE ? lds + P.numNodes * ldsNodeF4 * 4 : lds;
     int *const my = stk + threadIdx.x;
 
     const float4 *nodes = P.nodes, *tris = P.tris, *shade = P.shade;
-    constexpr int ldsNodeF4 = WIDE ? kLdsNode4F4 : kLdsNodeF4;
     if (LDS_SCENE) {
-        float4 *sNodes = reinterpret_cast<float4 *>(stk + (P.stackDepth + 1) * kMeshBlock);
-        float4 *sTris = sNodes + P.numNodes * ldsNodeF4;
+        float4 *sNodes = reinterpret_cast<float4 *>(lds);
+        float4 *sTris = reinterpret_cast<float4 *>(stk + (P.stackDepth + 1) * kMeshBlock);
         float4 *sShade = sTris + P.numTris * 3;
         if (WIDE) {
             for (int i = threadIdx.x; i < P.numNodes * kLdsNode4F4; i += kMeshBlock) sNodes[i] = P.nodes[i];
@@ -272,7 +275,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         do {
             prof<STATS>(pc, 2);
             if (WIDE)
-                traverse_round_wide<nodeF4, STATS, FULL, QUANT, SPILL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit,
+                traverse_round_wide<nodeF4, STATS, FULL, QUANT, SPILL, LDS_SCENE>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit,
                                                                 P.nodeExit, S);
             else
                 traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
@@ -411,6 +414,11 @@ hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hip
     if (p.wide && (p.stackCap < 1 || p.stackCap + 2 > p.stackDepth)) return hipErrorInvalidValue;
     const bool lds = p.ldsScene != 0;
     const size_t bytes = mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0, p.wide != 0);
+    const MeshFn fn = mesh_fn(countTraversal, lds, p.full != 0, p.wide != 0, p.wide == 2 && !lds, p.spill != nullptr);
+    if (lds && p.wide) {
+        const hipError_t e = check_lds_at_zero(reinterpret_cast<const void *>(fn));
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(mesh_fn(countTraversal, lds, p.full != 0, p.wide != 0, p.wide == 2 && !lds, p.spill != nullptr),
                        dim3(blocks),
                        dim3(kMeshBlock), bytes, s, p);

@@ -618,6 +618,16 @@ __device__ __forceinline__ float4 ld4(const float4 *base, unsigned byteOffset) {
     return *reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(base) + byteOffset);
 }
 
+// A 16-byte read at LDS byte address `a` (the kernels' dynamic LDS starts at address 0 and an
+// LDS-resident scene's nodes sit at its start): the address is the node row's offset itself.  The
+// compiler does not fold the dynamic LDS symbol's address (0) into the instruction, so a read
+// through the array costs an add (v_xad for the far row) per row.
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 lds_ld4(unsigned a) {
+    const f32x4 v = *reinterpret_cast<const __attribute__((address_space(3))) f32x4 *>(size_t(a));
+    return make_float4(v.x, v.y, v.z, v.w);
+}
+
 // Compare-exchange of (key, child code) pairs: afterwards ka <= kb.
 __device__ __forceinline__ void cas(unsigned &ka, int &ca, unsigned &kb, int &cb) {
     const bool sw = kb < ka;
@@ -632,7 +642,7 @@ __device__ __forceinline__ void cas(unsigned &ka, int &ca, unsigned &kb, int &cb
 // traverse_round over the 4-wide tree: a node visit tests its four child boxes, descends into
 // the nearest hit child and pushes the other hit children far to near.  SPILL=false: the tree's
 // stack bound fits the LDS capacity (no spill/refill code in the loop).
-template <int NODE_F4, bool STATS, bool FULL, bool QUANT = false, bool SPILL = true>
+template <int NODE_F4, bool STATS, bool FULL, bool QUANT = false, bool SPILL = true, bool LDS0 = false>
 __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *my, const float4 *nodes,
                                                     const float4 *tris, unsigned long long &nvis,
                                                     unsigned long long &ntest, unsigned *pc, unsigned leafExit,
@@ -652,10 +662,12 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
             // 128-byte float nodes (LDS and global): nb's low 7 bits are zero, so the octant's
             // near row is nb | s and the far row its ^ 16
             const unsigned ax = nb | sx, ay = nb | sy, az = nb | sz;
-            const float4 nx = ld4(nodes, ax), fx = ld4(nodes, ax ^ 16u);
-            const float4 ny = ld4(nodes, ay), fy = ld4(nodes, ay ^ 16u);
-            const float4 nz = ld4(nodes, az), fz = ld4(nodes, az ^ 16u);
-            ch = *reinterpret_cast<const int4 *>(reinterpret_cast<const char *>(nodes) + nb + 96u);
+            // LDS0: the nodes are the LDS scene copy at LDS address 0
+            const float4 nx = LDS0 ? lds_ld4(ax) : ld4(nodes, ax), fx = LDS0 ? lds_ld4(ax ^ 16u) : ld4(nodes, ax ^ 16u);
+            const float4 ny = LDS0 ? lds_ld4(ay) : ld4(nodes, ay), fy = LDS0 ? lds_ld4(ay ^ 16u) : ld4(nodes, ay ^ 16u);
+            const float4 nz = LDS0 ? lds_ld4(az) : ld4(nodes, az), fz = LDS0 ? lds_ld4(az ^ 16u) : ld4(nodes, az ^ 16u);
+            const float4 cw = LDS0 ? lds_ld4(nb + 96u) : ld4(nodes, nb + 96u);
+            ch = *reinterpret_cast<const int4 *>(&cw);
             k0 = child_key(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, r, tmin, T.bestT);
             k1 = child_key(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, r, tmin, T.bestT);
             k2 = child_key(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z, r, tmin, T.bestT);

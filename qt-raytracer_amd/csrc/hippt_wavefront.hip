@@ -100,9 +100,11 @@ __global__ void wf_init(WfParams W) {
 // WIDE: the megakernel's 4-wide traversal (QUANT: over 8-bit child boxes, global memory only).
 template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE, bool QUANT>
 __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
-    extern __shared__ int stk[];
-    int *const my = stk + threadIdx.x;
+    extern __shared__ int lds[];  // LDS scene: nodes at address 0, then stack, primitives
+    constexpr int ldsNodeF4 = WIDE ? kLdsNode4F4 : kLdsNodeF4;  // mesh_lds_bytes layout
     const MeshParams &P = W.mp;
+    int *const stk = LDS_SCENE ? lds + P.numNodes * ldsNodeF4 * 4 : lds;
+    int *const my = stk + threadIdx.x;
     const int qFirst = kCtrExt0 + cur * kWfShards;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
         // this iteration's rays = its segments; consume the generated work; shade/generate
@@ -117,10 +119,9 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
         }
     }
     const float4 *nodes = P.nodes, *tris = P.tris;
-    constexpr int ldsNodeF4 = WIDE ? kLdsNode4F4 : kLdsNodeF4;  // mesh_lds_bytes layout
     if (LDS_SCENE) {
-        float4 *sNodes = reinterpret_cast<float4 *>(stk + (P.stackDepth + 1) * kMeshBlock);
-        float4 *sTris = sNodes + P.numNodes * ldsNodeF4;
+        float4 *sNodes = reinterpret_cast<float4 *>(lds);
+        float4 *sTris = reinterpret_cast<float4 *>(stk + (P.stackDepth + 1) * kMeshBlock);
         if (WIDE) {
             for (int i = threadIdx.x; i < P.numNodes * kLdsNode4F4; i += kMeshBlock) sNodes[i] = P.nodes[i];
         } else {
@@ -174,7 +175,7 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
         if (!__any(busy(T))) break;
         do {
             if (WIDE)
-                traverse_round_wide<nodeF4, STATS, FULL, QUANT>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit,
+                traverse_round_wide<nodeF4, STATS, FULL, QUANT, true, LDS_SCENE>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit,
                                                                 P.nodeExit, S);
             else
                 traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
@@ -318,6 +319,11 @@ hipError_t wf_launch_extend(const WfParams &W, int cur, int blocks, bool countTr
     const MeshParams &P = W.mp;
     const bool lds = P.ldsScene != 0;
     const size_t bytes = mesh_lds_bytes(P.stackDepth, lds ? P.numNodes : 0, lds ? P.numTris : 0, P.wide != 0);
+    if (lds && P.wide) {
+        const hipError_t e = check_lds_at_zero(
+            reinterpret_cast<const void *>(ext_fn(countTraversal, lds, P.full != 0, P.wide != 0, false)));
+        if (e != hipSuccess) return e;
+    }
     hipLaunchKernelGGL(ext_fn(countTraversal, lds, P.full != 0, P.wide != 0, P.wide == 2 && !lds), dim3(blocks),
                        dim3(kMeshBlock), bytes, s, W, cur);
     return hipGetLastError();
