@@ -467,12 +467,30 @@ __device__ __forceinline__ void test_prim(Trav &T, const Ray &r, const float4 *t
 // One leaf-loop iteration for this lane: the primitives of leaf T.leaf, then the next leaf if it
 // is next in line on the stack.  (Measured and rejected: one primitive per lane per iteration,
 // so that lanes with short leaves move on: Cornell -9%, blob70k -5%.)
-template <bool STATS, bool FULL, typename Pop>
+template <bool STATS, bool FULL, typename Pop, bool PAIRS = false>
 __device__ __forceinline__ void leaf_step(Trav &T, const Ray &r, const float4 *tris, unsigned long long &ntest,
                                           unsigned *pc, Pop pop) {
     const int code = ~T.leaf;
     const int first = code >> 4, last = first + (code & 15);
-    for (int i = first; i < last; ++i) test_prim<STATS, FULL>(T, r, tris, i, ntest, pc);
+    if (PAIRS) {
+        // two primitives' loads in flight per iteration (trees in global memory: blob70k +3%;
+        // no gain from LDS)
+        for (int i = first; i < last; i += 2) {
+            const float4 *tp = tris + 3 * i;
+            const float4 A0 = tp[0], B0 = tp[1], C0 = tp[2];
+            const bool two = i + 1 < last;
+            float4 A1 = A0, B1 = B0, C1 = C0;
+            if (two) {
+                A1 = tp[3];
+                B1 = tp[4];
+                C1 = tp[5];
+            }
+            test_prim_data<STATS, FULL>(T, r, A0, B0, C0, i, ntest, pc);
+            if (two) test_prim_data<STATS, FULL>(T, r, A1, B1, C1, i + 1, ntest, pc);
+        }
+    } else {
+        for (int i = first; i < last; ++i) test_prim<STATS, FULL>(T, r, tris, i, ntest, pc);
+    }
     // a leaf that was next in line is processed in the same loop
     T.leaf = 0;
     if (T.cur < 0 && T.cur != kDone) {
@@ -724,9 +742,10 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
         }
         if (__popcll(__ballot((T.leaf | T.cur) >= 0)) <= leafExit) break;
     }
+    auto popw = [&] { return pop_wide<SPILL>(T, my, S); };
     while (T.leaf != 0) {
         prof<STATS>(pc, 4);
-        leaf_step<STATS, FULL>(T, r, tris, ntest, pc, [&] { return pop_wide<SPILL>(T, my, S); });
+        leaf_step<STATS, FULL, decltype(popw), !LDS0>(T, r, tris, ntest, pc, popw);
         if (nodeExit && __popcll(__ballot(T.leaf != 0)) <= nodeExit) break;
     }
 }
