@@ -645,12 +645,13 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         // trees an earlier one (blob70k 24: -3%)
                         p.waveThreshold = s.waveThreshold >= 0 ? s.waveThreshold : ldsScene ? 16 : 32;
                         p.chunk = s.chunk;
-                        // Loop exits of the traversal round (measured): deep L2/HBM-resident
-                        // trees leave the node loop once <= levels-6 lanes still search (blob70k,
-                        // 21 levels: 9.8 -> 12.5 G), LDS scenes at 4; every scene leaves the leaf loop
-                        // once <= 48 lanes hold a leaf (Cornell 28.4 -> 31.3 G, blob -> 13.4 G).
-                        p.leafExit = unsigned(s.leafExit >= 0 ? s.leafExit
-                                                              : ldsScene ? 4 : std::clamp(s.scene.levels - 6, 0, 16));
+                        // Loop exits of the traversal round (measured): trees in global
+                        // memory leave the node loop once <= 17 lanes still search for a leaf (r2
+                        // sweep of the 4-wide kernels: blob70k, 21 levels, best at 17-18; blob64x34
+                        // and random_scene, 16 and 12 levels, best at 15 — the round-1 rule
+                        // levels-6 gave 10 and 6, -3.7% and -1.6%), LDS scenes at 4; every scene
+                        // leaves the leaf loop once <= 48 lanes hold a leaf (Cornell 28.4 -> 31.3 G).
+                        p.leafExit = unsigned(s.leafExit >= 0 ? s.leafExit : ldsScene ? 4 : 17);
                         p.nodeExit = unsigned(s.nodeExit >= 0 ? s.nodeExit : 48);
                         p.wide = quant ? 2 : wide ? 1 : 0;
                         p.stackCap = stackCap;
