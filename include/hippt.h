@@ -201,11 +201,20 @@ enum {
                                        0 (default): 4-wide */
     , HIPPT_OPT_STACK_CAP = 18      /* 4-wide traversal: LDS stack entries per lane, 4..30 (deeper stacks spill
                                        to global memory); 0 (default): the tree's bound, at most 19 (30 for
-                                       LDS scenes) */
+                                       LDS scenes; 13 for a megakernel over a tree in global memory
+                                       whose bound exceeds 19, the rest of the LDS holding the top
+                                       of the tree) */
     , HIPPT_OPT_BVH_QUANT = 19      /* 4-wide traversal of global-memory trees over 64-byte nodes with 8-bit
                                        child boxes (1) or 128-byte float nodes (0); -1 (default): 8-bit for
-                                       Lambertian-triangle scenes */
+                                       the wavefront path's Lambertian-triangle scenes */
+    , HIPPT_OPT_LDS_TOP_NODES = 20  /* 4-wide traversal of global-memory trees: the top of the tree (this many
+                                       nodes, breadth-first) is copied into every block's LDS and read from
+                                       there; 0: none; -1 (default): automatic (what the LDS budget of the
+                                       resident blocks leaves beside the stack) */
 };
+/* Read-only (hipptGetOption) facts of the last megakernel render: LDS bytes of the top of the tree,
+ * persistent-grid blocks per CU. */
+enum { HIPPT_INFO_LDS_TOP_BYTES = 100, HIPPT_INFO_BLOCKS_PER_CU = 101 };
 bool hipptSetOption(int key, long long value);
 long long hipptGetOption(int key);
 /* BVH width (2 or 4) the last mesh render traversed (0 before any): what nodeVisits count. */

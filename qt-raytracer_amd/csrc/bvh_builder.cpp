@@ -389,6 +389,40 @@ void collapse_bvh4(const Bvh &bvh2, Bvh4 &out) {
     Collapser(bvh2, out).emit(0, 0, 1);
 }
 
+int order_bvh4_top(Bvh4 &b, int topNodes) {
+    const int n = int(b.nodes.size() / kNode4Words);
+    if (n == 0) return 0;
+    topNodes = std::max(1, std::min(topNodes, n));
+    // BFS from the root for the first topNodes nodes; the rest keep their (preorder) order
+    std::vector<int> newIdx(size_t(n), -1), bfs;
+    bfs.reserve(size_t(topNodes));
+    bfs.push_back(0);
+    newIdx[0] = 0;
+    for (size_t h = 0; h < bfs.size() && int(bfs.size()) < topNodes; ++h) {
+        const uint32_t *w = &b.nodes[size_t(bfs[h]) * kNode4Words];
+        for (int i = 0; i < 4 && int(bfs.size()) < topNodes; ++i) {
+            const int32_t c = int32_t(w[24 + i]);
+            if (c < 0) continue;
+            newIdx[size_t(c)] = int(bfs.size());
+            bfs.push_back(c);
+        }
+    }
+    int next = int(bfs.size());
+    for (int k = 0; k < n; ++k)
+        if (newIdx[size_t(k)] < 0) newIdx[size_t(k)] = next++;
+    std::vector<uint32_t> out(b.nodes.size());
+    for (int k = 0; k < n; ++k) {
+        uint32_t *d = &out[size_t(newIdx[size_t(k)]) * kNode4Words];
+        std::memcpy(d, &b.nodes[size_t(k) * kNode4Words], kNode4Words * sizeof(uint32_t));
+        for (int i = 0; i < 4; ++i) {
+            const int32_t c = int32_t(d[24 + i]);
+            if (c >= 0) d[24 + i] = uint32_t(newIdx[size_t(c)]);
+        }
+    }
+    b.nodes.swap(out);
+    return int(bfs.size());
+}
+
 void quantize_bvh4(const Bvh4 &in, std::vector<uint32_t> &out) {
     const size_t n = in.nodes.size() / kNode4Words;
     out.assign(n * kNode4QWords, 0u);

@@ -61,6 +61,12 @@ struct Bvh4 {
 };
 void collapse_bvh4(const Bvh &bvh2, Bvh4 &out);
 
+// Renumbers the nodes so that the first `topNodes` are the tree's top in breadth-first order
+// (node k's children come after it; any prefix of them is the shallowest nodes), the others
+// following in their previous order.  The kernels copy such a prefix into LDS for trees read from
+// global memory.  Returns the number of nodes ordered breadth-first.
+int order_bvh4_top(Bvh4 &b, int topNodes);
+
 // The 4-wide tree with 8-bit child boxes (Ylitie et al. 2017, "Efficient incoherent ray traversal
 // on GPUs through compressed wide BVHs", reduced to 4 children): 64-byte nodes, same node
 // indices, child codes and primitive order as Bvh4.  Words:

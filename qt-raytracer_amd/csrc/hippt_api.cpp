@@ -41,6 +41,11 @@ constexpr int kStatWords = 32;  // [0..3] hipptStats counters, [4..19] phase pro
 // 4-wide traversal: LDS stack content capacity for scenes outside LDS (19 + 3 spare entries =
 // 22 KB per 256-lane block: 7 blocks per CU in 160 KB).
 constexpr int kWideStackCap = 19;
+constexpr int kSpillStackCap = 13;
+// 4-wide trees are numbered breadth-first for their first kTopOrderNodes nodes, so that a prefix
+// of the node array is the top of the tree; trees read from global memory keep such a prefix in
+// LDS (HIPPT_OPT_LDS_TOP_NODES)
+constexpr int kTopOrderNodes = 1365;  // 6 complete levels
 constexpr size_t kQueueBytes = 8 * 32 * sizeof(unsigned);  // hippt_trace.h kQueues x kQueueStride
 
 struct EventPair {
@@ -128,6 +133,9 @@ struct State {
     int bvhWidth = 0;   // megakernel traversal over the 2- or 4-wide BVH; 0: 4-wide if it fits in LDS
     int stackCap = 0;   // 4-wide LDS stack entries (0: automatic)
     int bvhQuant = -1;  // 4-wide global-memory traversal over 8-bit child boxes (-1: automatic)
+    int ldsTopNodes = -1;  // top-of-tree nodes copied into LDS for global-memory trees (-1: automatic)
+    unsigned activeTopBytes = 0;  // of the last mesh render (hipptGetOption HIPPT_INFO_*)
+    int activeBlocksPerCu = 0;
     int activeWidth = 0;  // BVH width of the last mesh render (hipptActiveBvhWidth)
     int blocksPerCu = 0;
     bool ldsScene = true;
@@ -584,26 +592,55 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                                                         hippt::mesh_lds_scene_limit();
                 // LDS stack entries per lane: 2-wide = interior levels (+1 spare); 4-wide = the
                 // builder's exact bound up to kWideStackCap (+3 spare; deeper stacks spill their
-                // bottom half to global memory), so that 7 blocks of a big scene fit in LDS
-                const int capLimit = s.stackCap > 0 ? s.stackCap : ldsScene ? 30 : kWideStackCap;
+                // bottom half to global memory), so that 7 blocks of a big scene fit in LDS.  A
+                // megakernel over a tree in global memory whose bound exceeds kWideStackCap (it
+                // spills anyway) keeps kSpillStackCap entries and gives the rest of its LDS to the
+                // top of the tree (blob70k, float nodes: cap 19 + 4 top nodes 17.8 G, cap 13 + 52
+                // top nodes 20.4 G; caps 9-15 within 1%, 7: -3%; r2w)
+                const bool topTree = wide && !ldsScene && s.pathMode == 0;
+                const int capLimit = s.stackCap > 0 ? s.stackCap
+                                     : ldsScene     ? 30
+                                     : topTree && s.scene.stackBound4 > kWideStackCap ? kSpillStackCap
+                                                                                       : kWideStackCap;
                 const int stackCap = wide ? std::max(1, std::min(s.scene.stackBound4, capLimit)) : 0;
                 const int stackDepth = wide ? stackCap + 2 : std::max(1, s.scene.levels);
                 const bool spills = wide && s.scene.stackBound4 > stackCap;
                 // 8-bit child boxes for trees read from global memory: 64-byte nodes, 4 vector loads
                 // instead of 7 where the texture addresser bounds the traversal (blob70k: TA busy
-                // 84%, 15.6 -> 17.7 G).  Automatic for the Lambertian-triangle kernel only
-                // (random_scene, general kernel: 20.9 -> 18.5 G).
-                const bool quant = wide && !ldsScene && (s.bvhQuant == 1 || (s.bvhQuant == -1 && !s.scene.full));
+                // 84%, 15.6 -> 17.7 G).  Automatic for the wavefront's Lambertian-triangle kernel
+                // only: the megakernel reads the top of the tree (most of the visits) from LDS,
+                // where the float nodes need no decode (blob70k 19.0 G 8-bit, 20.4 G float, r2v).
+                const bool quant = wide && !ldsScene &&
+                                   (s.bvhQuant == 1 || (s.bvhQuant == -1 && !s.scene.full && s.pathMode == 1));
+                // The top of a global-memory tree in LDS (megakernel): the breadth-first prefix of
+                // the node array that the LDS budget of the resident blocks leaves beside the stack
+                // (automatic), or HIPPT_OPT_LDS_TOP_NODES nodes.
+                unsigned topBytes = 0;
+                if (topTree && s.ldsTopNodes != 0) {
+                    const size_t nodeBytes = quant ? 64 : 128;
+                    size_t n = size_t(std::min(numNodes, kTopOrderNodes));
+                    if (s.ldsTopNodes > 0) {
+                        n = std::min(n, size_t(s.ldsTopNodes));
+                    } else {
+                        const size_t stackBytes = hippt::mesh_lds_bytes(stackDepth, 0, 0, true);
+                        const size_t budget = hippt::mesh_lds_block_budget();
+                        n = std::min(n, budget > stackBytes ? (budget - stackBytes) / nodeBytes : 0);
+                    }
+                    topBytes = unsigned(n * nodeBytes);
+                }
                 const long long occKey =
-                    occupancy_key(s.scene.version, stackDepth, ldsScene, s.scene.full, wide, quant, spills);
+                    occupancy_key(s.scene.version, stackDepth, ldsScene, s.scene.full, wide, quant, spills) ^
+                    ((long long)topBytes << 40);
                 if (c.occKey != occKey) {
                     const int ln = ldsScene ? numNodes : 0, lt = ldsScene ? numTris : 0;
-                    c.meshBlocksPerCu[0] =
-                        hippt::mesh_blocks_per_cu(false, s.scene.full, wide, quant, stackDepth, ln, lt, spills);
-                    c.meshBlocksPerCu[1] =
-                        hippt::mesh_blocks_per_cu(true, s.scene.full, wide, quant, stackDepth, ln, lt, spills);
+                    c.meshBlocksPerCu[0] = hippt::mesh_blocks_per_cu(false, s.scene.full, wide, quant, stackDepth,
+                                                                     ln, lt, spills, topBytes);
+                    c.meshBlocksPerCu[1] = hippt::mesh_blocks_per_cu(true, s.scene.full, wide, quant, stackDepth,
+                                                                     ln, lt, spills, topBytes);
                     c.occKey = occKey;
                 }
+                s.activeTopBytes = topBytes;
+                s.activeBlocksPerCu = c.meshBlocksPerCu[cnt ? 1 : 0];
                 int bpc = s.blocksPerCu > 0 ? s.blocksPerCu : c.meshBlocksPerCu[cnt ? 1 : 0];
                 for (int b = 0; b < count; b += fpb) {
                     const int nf = std::min(fpb, count - b);
@@ -655,6 +692,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.nodeExit = unsigned(s.nodeExit >= 0 ? s.nodeExit : 48);
                         p.wide = quant ? 2 : wide ? 1 : 0;
                         p.stackCap = stackCap;
+                        p.topBytes = topBytes;
                         if (s.pathMode == 1) {
                             if (!run_wavefront(c, p, cnt, spills, s.scene.stackBound4 + 3, err)) return false;
                         } else {
@@ -811,6 +849,7 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
     std::memcpy(sc.nodes.data(), bvh.nodes.data(), bvh.nodes.size() * sizeof(uint32_t));
     hippt::Bvh4 bvh4;
     hippt::collapse_bvh4(bvh, bvh4);
+    hippt::order_bvh4_top(bvh4, kTopOrderNodes);
     sc.nodes4.assign(bvh4.nodes.size() / 4, float4{});
     std::memcpy(sc.nodes4.data(), bvh4.nodes.data(), bvh4.nodes.size() * sizeof(uint32_t));
     sc.numNodes4 = int(bvh4.nodes.size() / hippt::kNode4Words);
@@ -1208,6 +1247,10 @@ extern "C" bool hipptSetOption(int key, long long value) {
         if (value < -1 || value > 1) return false;
         s.bvhQuant = int(value);
         return true;
+    case HIPPT_OPT_LDS_TOP_NODES:
+        if (value < -1 || value > kTopOrderNodes) return false;
+        s.ldsTopNodes = int(value);
+        return true;
     default: return false;
     }
 }
@@ -1239,6 +1282,9 @@ extern "C" long long hipptGetOption(int key) {
     case HIPPT_OPT_BVH_WIDTH: return s.bvhWidth;
     case HIPPT_OPT_STACK_CAP: return s.stackCap;
     case HIPPT_OPT_BVH_QUANT: return s.bvhQuant;
+    case HIPPT_OPT_LDS_TOP_NODES: return s.ldsTopNodes;
+    case HIPPT_INFO_LDS_TOP_BYTES: return s.activeTopBytes;
+    case HIPPT_INFO_BLOCKS_PER_CU: return s.activeBlocksPerCu;
     default: return -1;
     }
 }
@@ -1261,6 +1307,7 @@ extern "C" hipptBvh *hipptBvhBuild(const float *verts, int numTris, float extent
         return nullptr;
     }
     hippt::collapse_bvh4(b->bvh, b->bvh4);
+    hippt::order_bvh4_top(b->bvh4, kTopOrderNodes);
     hippt::quantize_bvh4(b->bvh4, b->bvh4q);
     return b;
 }

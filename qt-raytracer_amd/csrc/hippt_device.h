@@ -59,6 +59,9 @@ struct MeshParams {
     int stackCap;
     int spillCap;
     int *spill;
+    // 4-wide trees in global memory: bytes of the node array's prefix (the top of the tree,
+    // breadth-first, bvh_builder.h order_bvh4_top) copied to LDS address 0 and read from there
+    unsigned topBytes;
 };
 
 // Running average + tonemap over a batch of per-sample radiances
@@ -89,8 +92,10 @@ hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hip
 hipError_t launch_combine(const CombineParams &p, hipStream_t s);
 // Resident mesh-kernel blocks per CU for a given LDS stack depth and LDS scene size.
 int mesh_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,
-                       int ldsTris, bool spill);
-size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide);
+                       int ldsTris, bool spill, unsigned topBytes = 0);
+size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide, unsigned topBytes = 0);
+// LDS bytes per block that keep the persistent grid's resident blocks within a CU's LDS
+size_t mesh_lds_block_budget();
 size_t mesh_lds_scene_limit();
 constexpr int kMeshBlock = 256;
 // LDS-resident scene copies: 2-wide nodes at an 80-byte stride, 4-wide nodes in the 128-byte

@@ -202,7 +202,10 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     // their byte offset alone: no base add per row read), then the stack, primitives, shading.
     extern __shared__ int lds[];
     constexpr int ldsNodeF4 = WIDE ? kLdsNode4F4 : kLdsNodeF4;
-    int *const stk = LDS_SCENE ? lds + P.numNodes * ldsNodeF4 * 4 : lds;
+    // Trees in global memory (4-wide): the top of the tree (P.topBytes of the node array) at LDS
+    // address 0, then the stack.
+    constexpr bool TOP = WIDE && !LDS_SCENE;
+    int *const stk = LDS_SCENE ? lds + P.numNodes * ldsNodeF4 * 4 : lds + (TOP ? (P.topBytes >> 2) : 0u);
     int *const my = stk + threadIdx.x;
 
     const float4 *nodes = P.nodes, *tris = P.tris, *shade = P.shade;
@@ -222,6 +225,11 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         nodes = sNodes;
         tris = sTris;
         shade = sShade;
+    }
+    if (TOP && P.topBytes) {
+        float4 *sTop = reinterpret_cast<float4 *>(lds);
+        for (unsigned i = threadIdx.x; i < (P.topBytes >> 4); i += kMeshBlock) sTop[i] = P.nodes[i];
+        __syncthreads();
     }
     constexpr int nodeF4 = LDS_SCENE ? ldsNodeF4 : (WIDE ? (QUANT ? 4 : 8) : 4);
     const SpillArea S{P.spill, (blockIdx.x * unsigned(kMeshBlock) + threadIdx.x) * unsigned(P.spillCap), P.stackCap};
@@ -275,8 +283,8 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         do {
             prof<STATS>(pc, 2);
             if (WIDE)
-                traverse_round_wide<nodeF4, STATS, FULL, QUANT, SPILL, LDS_SCENE>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit,
-                                                                P.nodeExit, S);
+                traverse_round_wide<nodeF4, STATS, FULL, QUANT, SPILL, LDS_SCENE, TOP>(
+                    T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit, S, P.topBytes);
             else
                 traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
         } while (__popcll(__ballot(busy(T))) > unsigned(P.waveThreshold));
@@ -377,9 +385,9 @@ hipError_t launch_sphere4(const Sphere4Params &p, hipStream_t s) {
 
 // Stack: one spare slot per lane above the deepest level for the speculative far-child
 // write; then (LDS_SCENE) the scene copy.
-size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide) {
+size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide, unsigned topBytes) {
     return size_t(stackDepth + 1) * kMeshBlock * sizeof(int) +
-           size_t(ldsNodes) * (wide ? kLdsNode4F4 : kLdsNodeF4) * 16 + size_t(ldsTris) * (3 + 1) * 16;
+           size_t(ldsNodes) * (wide ? kLdsNode4F4 : kLdsNodeF4) * 16 + size_t(ldsTris) * (3 + 1) * 16 + topBytes;
 }
 
 size_t mesh_lds_scene_limit() { return 24u << 10; }
@@ -387,6 +395,9 @@ size_t mesh_lds_scene_limit() { return 24u << 10; }
 // waves a SIMD holds under the SGPR budget: 800 SGPRs per SIMD, 16 of them reserved per wave
 // for the trap handler (one block = 4 waves = one wave per SIMD)
 static constexpr int kMaxResidentBlocks = 800 / (HIPPT_NUM_SGPR + 16) < 8 ? 800 / (HIPPT_NUM_SGPR + 16) : 8;
+
+// 160 KiB of LDS per CU shared by the resident blocks, in 512-byte allocation granules
+size_t mesh_lds_block_budget() { return (size_t(160u << 10) / kMaxResidentBlocks) & ~size_t(511); }
 
 using MeshFn = void (*)(MeshParams);
 // node formats: 2-wide, 4-wide float, 4-wide quantized (global memory only)
@@ -413,9 +424,11 @@ hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hip
     if (p.stackDepth < 1 || p.stackDepth > kStackDepth) return hipErrorInvalidValue;
     if (p.wide && (p.stackCap < 1 || p.stackCap + 2 > p.stackDepth)) return hipErrorInvalidValue;
     const bool lds = p.ldsScene != 0;
-    const size_t bytes = mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0, p.wide != 0);
+    if (p.topBytes && (lds || !p.wide || p.topBytes % (p.wide == 2 ? 64u : 128u) || p.topBytes > (unsigned(p.numNodes) << (p.wide == 2 ? 6 : 7))))
+        return hipErrorInvalidValue;
+    const size_t bytes = mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0, p.wide != 0, p.topBytes);
     const MeshFn fn = mesh_fn(countTraversal, lds, p.full != 0, p.wide != 0, p.wide == 2 && !lds, p.spill != nullptr);
-    if (lds && p.wide) {
+    if (p.wide && (lds || p.topBytes)) {
         const hipError_t e = check_lds_at_zero(reinterpret_cast<const void *>(fn));
         if (e != hipSuccess) return e;
     }
@@ -434,10 +447,10 @@ hipError_t launch_combine(const CombineParams &p, hipStream_t s) {
 }
 
 int mesh_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,
-                       int ldsTris, bool spill) {
+                       int ldsTris, bool spill, unsigned topBytes) {
     int n = 0;
     const bool lds = ldsNodes > 0;
-    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, wide);
+    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, wide, topBytes);
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &n, mesh_fn(countTraversal, lds, full, wide, quant && wide && !lds, spill), kMeshBlock, bytes);
     if (e != hipSuccess || n <= 0) n = 1;

@@ -185,8 +185,9 @@ __device__ __forceinline__ void wave_append(bool req, unsigned value, unsigned *
 // 0 outer iteration, 1 camera ray, 2 traversal round, 3 interior node loop, 4 leaf loop,
 // 5 primitive test, 6 shading, 7 unit-sphere rejection loop.  pc[kNhHist + h] (4-wide trees)
 // counts node visits with h = 0..4 hit children; pc[kNhHist + 5] those with none hit only
-// because of the closest hit found since the node was pushed (float 4-wide nodes).
-constexpr int kProfPhases = 8, kNhHist = 2 * kProfPhases, kProfSlots = kNhHist + 6;
+// because of the closest hit found since the node was pushed (float 4-wide nodes); pc[kTopVisits]
+// the visits served by the LDS copy of the top of a global-memory tree.
+constexpr int kProfPhases = 8, kNhHist = 2 * kProfPhases, kTopVisits = kNhHist + 6, kProfSlots = kNhHist + 7;
 template <bool STATS>
 __device__ __forceinline__ void prof(unsigned *pc, int k) {
     if (STATS) {
@@ -660,11 +661,17 @@ __device__ __forceinline__ void cas(unsigned &ka, int &ca, unsigned &kb, int &cb
 // traverse_round over the 4-wide tree: a node visit tests its four child boxes, descends into
 // the nearest hit child and pushes the other hit children far to near.  SPILL=false: the tree's
 // stack bound fits the LDS capacity (no spill/refill code in the loop).
-template <int NODE_F4, bool STATS, bool FULL, bool QUANT = false, bool SPILL = true, bool LDS0 = false>
+// TOP (trees in global memory): the first topBytes of the node array (the top of the tree,
+// breadth-first) also sit at LDS address 0; a visit to one of them reads LDS, which spares the
+// texture addresser (TA) — the unit that bounds the traversal of global-memory trees — the loads
+// every ray makes at the top of the tree.
+template <int NODE_F4, bool STATS, bool FULL, bool QUANT = false, bool SPILL = true, bool LDS0 = false,
+          bool TOP = false>
 __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *my, const float4 *nodes,
                                                     const float4 *tris, unsigned long long &nvis,
                                                     unsigned long long &ntest, unsigned *pc, unsigned leafExit,
-                                                    unsigned nodeExit, const SpillArea &S) {
+                                                    unsigned nodeExit, const SpillArea &S,
+                                                    unsigned topBytes = 0) {
     const float tmin = 0.001f;
     // near-row byte offsets of this ray's octant within a node (x at 0/16, y at 32/48, z at 64/80)
     const unsigned sx = near_row(r.ix), sy = near_row(r.iy) | 32u, sz = near_row(r.iz) | 64u;
@@ -681,10 +688,24 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
             // near row is nb | s and the far row its ^ 16
             const unsigned ax = nb | sx, ay = nb | sy, az = nb | sz;
             // LDS0: the nodes are the LDS scene copy at LDS address 0
-            const float4 nx = LDS0 ? lds_ld4(ax) : ld4(nodes, ax), fx = LDS0 ? lds_ld4(ax ^ 16u) : ld4(nodes, ax ^ 16u);
-            const float4 ny = LDS0 ? lds_ld4(ay) : ld4(nodes, ay), fy = LDS0 ? lds_ld4(ay ^ 16u) : ld4(nodes, ay ^ 16u);
-            const float4 nz = LDS0 ? lds_ld4(az) : ld4(nodes, az), fz = LDS0 ? lds_ld4(az ^ 16u) : ld4(nodes, az ^ 16u);
-            const float4 cw = LDS0 ? lds_ld4(nb + 96u) : ld4(nodes, nb + 96u);
+            float4 nx, fx, ny, fy, nz, fz, cw;
+            if (LDS0 || (TOP && nb < topBytes)) {
+                nx = lds_ld4(ax);
+                fx = lds_ld4(ax ^ 16u);
+                ny = lds_ld4(ay);
+                fy = lds_ld4(ay ^ 16u);
+                nz = lds_ld4(az);
+                fz = lds_ld4(az ^ 16u);
+                cw = lds_ld4(nb + 96u);
+            } else {
+                nx = ld4(nodes, ax);
+                fx = ld4(nodes, ax ^ 16u);
+                ny = ld4(nodes, ay);
+                fy = ld4(nodes, ay ^ 16u);
+                nz = ld4(nodes, az);
+                fz = ld4(nodes, az ^ 16u);
+                cw = ld4(nodes, nb + 96u);
+            }
             ch = *reinterpret_cast<const int4 *>(&cw);
             k0 = child_key(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, r, tmin, T.bestT);
             k1 = child_key(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, r, tmin, T.bestT);
@@ -700,10 +721,20 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
         } else {
             // 64-byte node (bvh_builder.h quantize_bvh4): 4 loads instead of 7.  Plane q of axis
             // a enters the slab test as t = q*(s*inv) + (o*inv - o_ray*inv).
-            const float4 o = ld4(nodes, nb);
-            const uint4 q = *reinterpret_cast<const uint4 *>(reinterpret_cast<const char *>(nodes) + nb + 16u);
-            const float4 q2 = ld4(nodes, nb + 32u);
-            ch = *reinterpret_cast<const int4 *>(reinterpret_cast<const char *>(nodes) + nb + 48u);
+            float4 o, qf, q2, cw;
+            if (TOP && nb < topBytes) {
+                o = lds_ld4(nb);
+                qf = lds_ld4(nb + 16u);
+                q2 = lds_ld4(nb + 32u);
+                cw = lds_ld4(nb + 48u);
+            } else {
+                o = ld4(nodes, nb);
+                qf = ld4(nodes, nb + 16u);
+                q2 = ld4(nodes, nb + 32u);
+                cw = ld4(nodes, nb + 48u);
+            }
+            const uint4 q = *reinterpret_cast<const uint4 *>(&qf);
+            ch = *reinterpret_cast<const int4 *>(&cw);
             const float bx = o.w * r.ix, ax = fmaf(o.x, r.ix, -r.oix);
             const float by = q2.z * r.iy, ay = fmaf(o.y, r.iy, -r.oiy);
             const float bz = q2.w * r.iz, az = fmaf(o.z, r.iz, -r.oiz);
@@ -718,6 +749,7 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
             k3 = child_key_q<3>(nxw, fxw, nyw, fyw, nzw, fzw, ax, bx, ay, by, az, bz, tmin, T.bestT);
         }
         if (STATS) ++nvis;
+        if (STATS && TOP && nb < topBytes) ++pc[kTopVisits];
         // hit children: a miss key is all ones (bit 31), a hit key a positive float's bits
         const int nh = 4 - int((k0 >> 31) + (k1 >> 31) + (k2 >> 31) + (k3 >> 31));
         if (STATS) ++pc[kNhHist + nh];

@@ -44,6 +44,9 @@ OPT_BVH_SAH = 16
 OPT_BVH_WIDTH = 17
 OPT_STACK_CAP = 18
 OPT_BVH_QUANT = 19
+OPT_LDS_TOP_NODES = 20
+INFO_LDS_TOP_BYTES = 100
+INFO_BLOCKS_PER_CU = 101
 
 # Every symbol include/hippt.h declares (checked by tests/test_abi_cpu.py).
 EXPORTS = (
@@ -433,6 +436,8 @@ class PathTracer:
         out["hit_children"] = v[20:25]
         # of the visits with none hit: those with a child box hit before the closest-hit cut
         out["culled_by_best_t"] = v[25]
+        # node visits served by the LDS copy of the top of a global-memory tree
+        out["lds_top_visits"] = v[26] if len(v) > 26 else 0
         return out
 
     def resetStats(self) -> None:  # noqa: N802

@@ -27,7 +27,7 @@ def pt():
                  (hippt.OPT_COUNT_TRAVERSAL, 0), (hippt.OPT_BLOCKS_PER_CU, 0), (hippt.OPT_LDS_SCENE, 1),
                  (hippt.OPT_PATH_MODE, 0), (hippt.OPT_WAVEFRONT_SLOTS, 1 << 24), (hippt.OPT_LEAF_EXIT, -1),
                  (hippt.OPT_NODE_EXIT, -1), (hippt.OPT_BVH_SAH, 1), (hippt.OPT_BVH_WIDTH, 0),
-                 (hippt.OPT_STACK_CAP, 0), (hippt.OPT_BVH_QUANT, -1)):
+                 (hippt.OPT_STACK_CAP, 0), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_LDS_TOP_NODES, -1)):
         t.setOption(k, v)
     t.resetStats()
     yield t
@@ -310,6 +310,41 @@ def test_bvh_width_and_stack_spill_do_not_change_results(pt, name):
             assert pt.renderFrames(3, 8)
             got = pt.readback()
             _assert_same(got[0], got[1], ora[0], ora[1])
+
+
+@pytest.mark.parametrize("name", ["blob70k", "random_scene", "cornell34"])
+def test_lds_top_of_tree_does_not_change_results(pt, name):
+    """Trees read from global memory with the top of the tree copied into LDS
+    (HIPPT_OPT_LDS_TOP_NODES: none, the root alone, 5 and 85 nodes, the automatic size, which
+    covers all of cornell34's 16 nodes), float and 8-bit nodes, the spilling LDS stack (cap 4)
+    and the default: the oracle's image bit for bit.  Counting builds report LDS-served visits
+    exactly when a top is in LDS."""
+    sc = scenes.get_scene(name)
+    pt.uploadMesh(sc)
+    pt.setOption(hippt.OPT_LDS_SCENE, 0)
+    w, h = (40, 24) if name == "random_scene" else (56, 40)
+    ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
+    quants = (0,) if name == "random_scene" else (0, 1)
+    for quant in quants:
+        for cap in (0, 4):
+            for top in (0, 1, 5, 85, -1):
+                pt.setOption(hippt.OPT_BVH_QUANT, quant)
+                pt.setOption(hippt.OPT_STACK_CAP, cap)
+                pt.setOption(hippt.OPT_LDS_TOP_NODES, top)
+                assert pt.initialize(w, h)
+                pt.setOption(hippt.OPT_COUNT_TRAVERSAL, top in (0, -1))
+                pt.resetStats()
+                assert pt.renderFrames(3, 8)
+                got = pt.readback()
+                _assert_same(got[0], got[1], ora[0], ora[1])
+                if top in (0, -1):
+                    c = pt.counters()
+                    top_bytes = pt._lib.hipptGetOption(hippt.INFO_LDS_TOP_BYTES)
+                    assert (c["lds_top_visits"] > 0) == (top_bytes > 0), (quant, cap, top, top_bytes)
+                    assert c["lds_top_visits"] <= c["nodeVisits"]
+                    if top == 0:
+                        assert top_bytes == 0
+                pt.setOption(hippt.OPT_COUNT_TRAVERSAL, 0)
 
 
 @pytest.mark.parametrize("mode", [0, 1])

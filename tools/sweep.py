@@ -27,7 +27,7 @@ KEYS = {"wave": hippt.OPT_WAVE_THRESHOLD, "chunk": hippt.OPT_CHUNK, "scratch": h
         "depth": hippt.OPT_BVH_MAX_DEPTH, "leafexit": hippt.OPT_LEAF_EXIT,
         "nodeexit": hippt.OPT_NODE_EXIT, "sah": hippt.OPT_BVH_SAH,
         "width": hippt.OPT_BVH_WIDTH, "stackcap": hippt.OPT_STACK_CAP,
-        "quant": hippt.OPT_BVH_QUANT}
+        "quant": hippt.OPT_BVH_QUANT, "top": hippt.OPT_LDS_TOP_NODES}
 REUPLOAD = {"leaf", "tcost", "depth", "sah"}  # build parameters: take effect at the next upload
 
 
@@ -83,7 +83,9 @@ def main():
                           "trace_ms_step": round(st["traceMs"] / a.steps, 3),
                           "combine_ms_step": round(st["combineMs"] / a.steps, 3),
                           "launches_step": st["traceLaunches"] // a.steps, "bvh_nodes": st["bvhNodes"],
-                          "bvh_depth": st["bvhDepth"], **extra}), flush=True)
+                          "bvh_depth": st["bvhDepth"],
+                          "lds_top_bytes": pt._lib.hipptGetOption(hippt.INFO_LDS_TOP_BYTES),
+                          "blocks_per_cu": pt._lib.hipptGetOption(hippt.INFO_BLOCKS_PER_CU), **extra}), flush=True)
 
 
 if __name__ == "__main__":
