@@ -472,13 +472,17 @@ bool run_wavefront(Ctx &c, hippt::MeshParams p, bool cnt, bool spills, int spill
     W.extQ1 = queues + size_t(hippt::kWfShards) * shardCap;
     W.genQ = queues + 2 * size_t(hippt::kWfShards) * shardCap;
     const bool wide = p.wide != 0, quant = p.wide == 2;
-    const long long occKey = occupancy_key(s.scene.version, p.stackDepth, p.ldsScene != 0, p.full != 0, wide, quant);
+    const long long occKey = occupancy_key(s.scene.version, p.stackDepth, p.ldsScene != 0, p.full != 0, wide, quant) ^
+                             ((long long)p.topBytes << 40);
     if (c.wfOccKey != occKey) {
         const int ln = p.ldsScene ? p.numNodes : 0, lt = p.ldsScene ? p.numTris : 0;
-        c.wfBlocksPerCu[0] = hippt::wf_extend_blocks_per_cu(false, p.full != 0, wide, quant, p.stackDepth, ln, lt);
-        c.wfBlocksPerCu[1] = hippt::wf_extend_blocks_per_cu(true, p.full != 0, wide, quant, p.stackDepth, ln, lt);
+        c.wfBlocksPerCu[0] =
+            hippt::wf_extend_blocks_per_cu(false, p.full != 0, wide, quant, p.stackDepth, ln, lt, p.topBytes);
+        c.wfBlocksPerCu[1] =
+            hippt::wf_extend_blocks_per_cu(true, p.full != 0, wide, quant, p.stackDepth, ln, lt, p.topBytes);
         c.wfOccKey = occKey;
     }
+    s.activeBlocksPerCu = c.wfBlocksPerCu[cnt ? 1 : 0];
     const int bpc = s.blocksPerCu > 0 ? s.blocksPerCu : c.wfBlocksPerCu[cnt ? 1 : 0];
     const int blocks = int(std::max(1LL, std::min<long long>((long long)c.cus * bpc, (slots + 255) / 256)));
     if (!ensure_spill(c, p, blocks, spills, spillCap, err)) return false;
@@ -593,11 +597,11 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 // LDS stack entries per lane: 2-wide = interior levels (+1 spare); 4-wide = the
                 // builder's exact bound up to kWideStackCap (+3 spare; deeper stacks spill their
                 // bottom half to global memory), so that 7 blocks of a big scene fit in LDS.  A
-                // megakernel over a tree in global memory whose bound exceeds kWideStackCap (it
+                // traversal of a tree in global memory whose bound exceeds kWideStackCap (it
                 // spills anyway) keeps kSpillStackCap entries and gives the rest of its LDS to the
                 // top of the tree (blob70k, float nodes: cap 19 + 4 top nodes 17.8 G, cap 13 + 52
                 // top nodes 20.4 G; caps 9-15 within 1%, 7: -3%; r2w)
-                const bool topTree = wide && !ldsScene && s.pathMode == 0;
+                const bool topTree = wide && !ldsScene;
                 const int capLimit = s.stackCap > 0 ? s.stackCap
                                      : ldsScene     ? 30
                                      : topTree && s.scene.stackBound4 > kWideStackCap ? kSpillStackCap
@@ -608,13 +612,14 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 // 8-bit child boxes for trees read from global memory: 64-byte nodes, 4 vector loads
                 // instead of 7 where the texture addresser bounds the traversal (blob70k: TA busy
                 // 84%, 15.6 -> 17.7 G).  Automatic for the wavefront's Lambertian-triangle kernel
-                // only: the megakernel reads the top of the tree (most of the visits) from LDS,
+                // only: the megakernel reads the top of the tree (62-70% of the visits) from LDS,
                 // where the float nodes need no decode (blob70k 19.0 G 8-bit, 20.4 G float, r2v).
                 const bool quant = wide && !ldsScene &&
                                    (s.bvhQuant == 1 || (s.bvhQuant == -1 && !s.scene.full && s.pathMode == 1));
-                // The top of a global-memory tree in LDS (megakernel): the breadth-first prefix of
-                // the node array that the LDS budget of the resident blocks leaves beside the stack
-                // (automatic), or HIPPT_OPT_LDS_TOP_NODES nodes.
+                // The top of a global-memory tree in LDS (megakernel and wavefront extend): the
+                // breadth-first prefix of the node array that the LDS budget of the resident blocks
+                // leaves beside the stack (automatic), or HIPPT_OPT_LDS_TOP_NODES nodes.  The
+                // wavefront keeps its 8-bit nodes (blob70k: 8.28 G 8-bit, 7.53 G float, r2za).
                 unsigned topBytes = 0;
                 if (topTree && s.ldsTopNodes != 0) {
                     const size_t nodeBytes = quant ? 64 : 128;

@@ -49,6 +49,6 @@ hipError_t wf_launch_generate(const WfParams &W, int nxt, bool countSamples, hip
 hipError_t wf_launch_extend(const WfParams &W, int cur, int blocks, bool countTraversal, hipStream_t s);
 hipError_t wf_launch_shade(const WfParams &W, int cur, hipStream_t s);
 int wf_extend_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,
-                            int ldsTris);
+                            int ldsTris, unsigned topBytes = 0);
 
 }  // namespace hippt

@@ -103,7 +103,9 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
     extern __shared__ int lds[];  // LDS scene: nodes at address 0, then stack, primitives
     constexpr int ldsNodeF4 = WIDE ? kLdsNode4F4 : kLdsNodeF4;  // mesh_lds_bytes layout
     const MeshParams &P = W.mp;
-    int *const stk = LDS_SCENE ? lds + P.numNodes * ldsNodeF4 * 4 : lds;
+    // trees in global memory: the top of the tree (P.topBytes) at LDS address 0, then the stack
+    constexpr bool TOP = WIDE && !LDS_SCENE;
+    int *const stk = LDS_SCENE ? lds + P.numNodes * ldsNodeF4 * 4 : lds + (TOP ? (P.topBytes >> 2) : 0u);
     int *const my = stk + threadIdx.x;
     const int qFirst = kCtrExt0 + cur * kWfShards;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -132,6 +134,11 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
         __syncthreads();
         nodes = sNodes;
         tris = sTris;
+    }
+    if (TOP && P.topBytes) {
+        float4 *sTop = reinterpret_cast<float4 *>(lds);
+        for (unsigned i = threadIdx.x; i < (P.topBytes >> 4); i += kMeshBlock) sTop[i] = P.nodes[i];
+        __syncthreads();
     }
     constexpr int nodeF4 = WIDE ? (QUANT ? 4 : (LDS_SCENE ? kLdsNode4F4 : 8)) : (LDS_SCENE ? kLdsNodeF4 : 4);
     const SpillArea S{P.spill, (blockIdx.x * unsigned(kMeshBlock) + threadIdx.x) * unsigned(P.spillCap), P.stackCap};
@@ -175,8 +182,8 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
         if (!__any(busy(T))) break;
         do {
             if (WIDE)
-                traverse_round_wide<nodeF4, STATS, FULL, QUANT, true, LDS_SCENE>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit,
-                                                                P.nodeExit, S);
+                traverse_round_wide<nodeF4, STATS, FULL, QUANT, true, LDS_SCENE, TOP>(
+                    T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit, S, P.topBytes);
             else
                 traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
         } while (__popcll(__ballot(busy(T))) > unsigned(P.waveThreshold));
@@ -318,8 +325,11 @@ hipError_t wf_launch_generate(const WfParams &W, int nxt, bool countSamples, hip
 hipError_t wf_launch_extend(const WfParams &W, int cur, int blocks, bool countTraversal, hipStream_t s) {
     const MeshParams &P = W.mp;
     const bool lds = P.ldsScene != 0;
-    const size_t bytes = mesh_lds_bytes(P.stackDepth, lds ? P.numNodes : 0, lds ? P.numTris : 0, P.wide != 0);
-    if (lds && P.wide) {
+    if (P.topBytes && (lds || !P.wide || P.topBytes % (P.wide == 2 ? 64u : 128u) ||
+                       P.topBytes > (unsigned(P.numNodes) << (P.wide == 2 ? 6 : 7))))
+        return hipErrorInvalidValue;
+    const size_t bytes = mesh_lds_bytes(P.stackDepth, lds ? P.numNodes : 0, lds ? P.numTris : 0, P.wide != 0, P.topBytes);
+    if (P.wide && (lds || P.topBytes)) {
         const hipError_t e = check_lds_at_zero(
             reinterpret_cast<const void *>(ext_fn(countTraversal, lds, P.full != 0, P.wide != 0, false)));
         if (e != hipSuccess) return e;
@@ -335,9 +345,9 @@ hipError_t wf_launch_shade(const WfParams &W, int cur, hipStream_t s) {
 }
 
 int wf_extend_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,
-                            int ldsTris) {
+                            int ldsTris, unsigned topBytes) {
     int n = 0;
-    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, wide);
+    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, wide, topBytes);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(
             &n, ext_fn(countTraversal, ldsNodes > 0, full, wide, quant && wide && ldsNodes == 0), kMeshBlock, bytes) !=
             hipSuccess ||
