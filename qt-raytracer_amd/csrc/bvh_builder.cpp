@@ -380,13 +380,197 @@ private:
     Bvh4 &out_;
 };
 
+// SAH-optimal collapse (dynamic programming over the 2-wide tree, after Ylitie et al. 2017,
+// reduced to 4 children): cost(n, i) = least expected cost of the 2-wide subtree n spread over
+// at most i child slots of its 4-wide parent, where a slot is a leaf of at most maxLeaf
+// primitives (a 2-wide subtree's primitives are contiguous, so any subtree can become one leaf:
+// area * count * 1), a 4-wide node (area * nodeCost + its children's cost over 4 slots), or,
+// for i > 1, the subtree's two children sharing the slots.  Areas are relative to the root's.
+class SahCollapser {
+public:
+    SahCollapser(const Bvh &b, Bvh4 &o, float nodeCost, int maxLeaf)
+        : in_(b), out_(o), cn_(nodeCost), maxLeaf_(std::max(1, std::min(maxLeaf, 15))) {
+        const size_t n = in_.nodes.size() / kNodeWords;
+        dp_.assign(n, Dp{});
+        std::vector<int> order;  // preorder; children after parents -> reverse is bottom-up
+        order.reserve(n);
+        order.push_back(0);
+        for (size_t h = 0; h < order.size(); ++h)
+            for (int c = 0; c < 2; ++c) {
+                const int32_t k = code(order[h], c);
+                if (k >= 0) order.push_back(k);
+            }
+        for (size_t h = order.size(); h-- > 0;) solve(order[h]);
+    }
+
+    // Emits the 4-wide node for 2-wide node `node`; returns its index.
+    int emit(int node, int pushesAbove, int level) {
+        Slot slots[4];
+        int n = 0;
+        const Dp &d = dp_[size_t(node)];
+        expand_child(node, 0, d.splitD4, slots, n);
+        expand_child(node, 1, 4 - d.splitD4, slots, n);
+        const int idx = int(out_.nodes.size() / kNode4Words);
+        out_.nodes.resize(out_.nodes.size() + kNode4Words, 0u);
+        out_.levels = std::max(out_.levels, level);
+        const int pushes = pushesAbove + (n - 1);
+        out_.stackBound = std::max(out_.stackBound, pushes);
+        int32_t codes[4];
+        for (int i = 0; i < 4; ++i) codes[i] = i < n ? slots[i].code : leaf_code(0, 0);
+        for (int i = 0; i < n; ++i)
+            if (slots[i].code >= 0) codes[i] = emit(slots[i].code, pushes, level + 1);
+        float f[24];
+        for (int i = 0; i < 4; ++i)
+            for (int a = 0; a < 3; ++a) {
+                f[8 * a + i] = i < n ? slots[i].lo[a] : kFar[a];
+                f[8 * a + 4 + i] = i < n ? slots[i].hi[a] : kFar[a];
+            }
+        uint32_t *dst = &out_.nodes[size_t(idx) * kNode4Words];
+        std::memcpy(dst, f, sizeof(f));
+        for (int i = 0; i < 4; ++i) dst[24 + i] = uint32_t(codes[i]);
+        return idx;
+    }
+
+private:
+    struct Dp {
+        float cost[5] = {0, 0, 0, 0, 0};  // cost(n, i), i = 1..4
+        bool leaf = false;                // cost(n, 1) is the merged leaf (else a 4-wide node)
+        bool spread[5] = {};              // cost(n, i) spreads the two children over i slots
+        int split[5] = {};                // slots of child 0 when spread (i = 2..4)
+        int splitD4 = 2;                  // child 0's slots in the 4-wide node's distribution
+        int first = 0, count = 0;         // contiguous primitive range (count < 0: not contiguous)
+    };
+
+    int32_t code(int node, int c) const { return int32_t(in_.nodes[size_t(node) * kNodeWords + 12 + size_t(c)]); }
+
+    void box(int node, int c, float *lo, float *hi) const {
+        float f[12];
+        std::memcpy(f, &in_.nodes[size_t(node) * kNodeWords], sizeof(f));
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = f[6 * c + a];
+            hi[a] = f[6 * c + 3 + a];
+        }
+    }
+
+    static float area(const float *lo, const float *hi) {
+        const float dx = hi[0] - lo[0], dy = hi[1] - lo[1], dz = hi[2] - lo[2];
+        if (dx < 0 || dy < 0 || dz < 0) return 0.0f;
+        return 2.0f * (dx * dy + dy * dz + dz * dx);
+    }
+
+    // cost(child c of node, i), its primitive range and whether it is a 2-wide leaf
+    void child(int node, int c, int i, float &cost, int &first, int &count) const {
+        const int32_t k = code(node, c);
+        if (k >= 0) {
+            cost = dp_[size_t(k)].cost[i];
+            first = dp_[size_t(k)].first;
+            count = dp_[size_t(k)].count;
+            return;
+        }
+        float lo[3], hi[3];
+        box(node, c, lo, hi);
+        first = (~k) >> 4;
+        count = (~k) & 15;
+        cost = area(lo, hi) * float(count) / rootArea();
+    }
+
+    float rootArea() const {
+        if (rootArea_ > 0) return rootArea_;
+        float lo0[3], hi0[3], lo1[3], hi1[3], lo[3], hi[3];
+        box(0, 0, lo0, hi0);
+        box(0, 1, lo1, hi1);
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo0[a], lo1[a]);
+            hi[a] = std::max(hi0[a], hi1[a]);
+        }
+        rootArea_ = std::max(area(lo, hi), 1e-30f);
+        return rootArea_;
+    }
+
+    void solve(int node) {
+        Dp &d = dp_[size_t(node)];
+        float lo0[3], hi0[3], lo1[3], hi1[3], lo[3], hi[3];
+        box(node, 0, lo0, hi0);
+        box(node, 1, lo1, hi1);
+        for (int a = 0; a < 3; ++a) {
+            lo[a] = std::min(lo0[a], lo1[a]);
+            hi[a] = std::max(hi0[a], hi1[a]);
+        }
+        const float an = area(lo, hi) / rootArea();
+        float c0[5], c1[5];
+        int f0 = 0, n0 = 0, f1 = 0, n1 = 0;
+        for (int i = 1; i <= 4; ++i) {
+            child(node, 0, i, c0[i], f0, n0);
+            child(node, 1, i, c1[i], f1, n1);
+        }
+        // the subtree's primitives as one range (the builder partitions in place)
+        if (n0 >= 0 && n1 >= 0 && (n0 == 0 || n1 == 0 || f0 + n0 == f1)) {
+            d.first = n0 == 0 ? f1 : f0;
+            d.count = n0 + n1;
+        } else {
+            d.count = -1;
+        }
+        float D[5] = {0, INFINITY, INFINITY, INFINITY, INFINITY};
+        int Ds[5] = {0, 0, 1, 1, 2};
+        for (int j = 2; j <= 4; ++j)
+            for (int k = 1; k < j; ++k) {
+                const float c = c0[k] + c1[j - k];
+                if (c < D[j]) {
+                    D[j] = c;
+                    Ds[j] = k;
+                }
+            }
+        d.splitD4 = Ds[4];
+        const float asNode = an * cn_ + D[4];
+        const float asLeaf = d.count >= 0 && d.count <= maxLeaf_ ? an * float(d.count) : INFINITY;
+        d.leaf = asLeaf <= asNode;
+        d.cost[1] = std::min(asLeaf, asNode);
+        for (int i = 2; i <= 4; ++i) {
+            d.spread[i] = D[i] < d.cost[1];
+            d.split[i] = Ds[i];
+            d.cost[i] = std::min(d.cost[1], D[i]);
+        }
+    }
+
+    // Appends the slots that child c of `node` becomes when given `i` slots.
+    void expand_child(int node, int c, int i, Slot *slots, int &n) const {
+        const int32_t k = code(node, c);
+        if (k < 0) {
+            Slot &sl = slots[n++];
+            box(node, c, sl.lo, sl.hi);
+            sl.code = k;
+            return;
+        }
+        const Dp &d = dp_[size_t(k)];
+        if (i > 1 && d.spread[i]) {
+            expand_child(k, 0, d.split[i], slots, n);
+            expand_child(k, 1, i - d.split[i], slots, n);
+            return;
+        }
+        Slot &sl = slots[n++];
+        box(node, c, sl.lo, sl.hi);
+        sl.code = d.leaf ? leaf_code(d.first, d.count) : k;
+    }
+
+    static constexpr float kFar[3] = {3.0e38f, -1.0e20f, 7.0e33f};
+    const Bvh &in_;
+    Bvh4 &out_;
+    float cn_;
+    int maxLeaf_;
+    std::vector<Dp> dp_;
+    mutable float rootArea_ = 0.0f;
+};
+
 }  // namespace
 
-void collapse_bvh4(const Bvh &bvh2, Bvh4 &out) {
+void collapse_bvh4(const Bvh &bvh2, Bvh4 &out, const BvhParams &params) {
     out.nodes.clear();
     out.levels = 0;
     out.stackBound = 0;
-    Collapser(bvh2, out).emit(0, 0, 1);
+    if (params.collapse == 1 && !bvh2.nodes.empty())
+        SahCollapser(bvh2, out, params.nodeCost, params.maxLeaf4).emit(0, 0, 1);
+    else
+        Collapser(bvh2, out).emit(0, 0, 1);
 }
 
 int order_bvh4_top(Bvh4 &b, int topNodes) {

@@ -27,6 +27,12 @@ struct BvhParams {
     float traversalCost = 1.0f;
     int maxDepth = kStackDepth;
     int sahMode = 1;  // 0: 16 bins on the longest centroid axis; 1: all axes, exact sweep (32 bins on big nodes)
+    // 4-wide collapse: 0 opens the largest-area interior child until a node has 4 children; 1 the
+    // SAH-optimal collapse (nodeCost = a 4-wide node visit in primitive tests; leaves may merge
+    // 2-wide subtrees up to maxLeaf4 primitives)
+    int collapse = 0;
+    float nodeCost = 2.0f;
+    int maxLeaf4 = 4;
 };
 
 struct Bvh {
@@ -59,7 +65,7 @@ struct Bvh4 {
     int stackBound = 0;           // most entries a traversal stack can hold: max over nodes of
                                   // the (children - 1) pushes of it and its ancestors
 };
-void collapse_bvh4(const Bvh &bvh2, Bvh4 &out);
+void collapse_bvh4(const Bvh &bvh2, Bvh4 &out, const BvhParams &params = BvhParams());
 
 // Renumbers the nodes so that the first `topNodes` are the tree's top in breadth-first order
 // (node k's children come after it; any prefix of them is the shallowest nodes), the others

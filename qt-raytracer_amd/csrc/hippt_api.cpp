@@ -134,6 +134,8 @@ struct State {
     int stackCap = 0;   // 4-wide LDS stack entries (0: automatic)
     int bvhQuant = -1;  // 4-wide global-memory traversal over 8-bit child boxes (-1: automatic)
     int ldsTopNodes = -1;  // top-of-tree nodes copied into LDS for global-memory trees (-1: automatic)
+    bool rngTable = false;  // memoized random_in_unit_sphere (HIPPT_OPT_RNG_TABLE)
+    std::vector<std::pair<int, uint32_t *>> rngTables;  // per device, built on first use
     unsigned activeTopBytes = 0;  // of the last mesh render (hipptGetOption HIPPT_INFO_*)
     int activeBlocksPerCu = 0;
     int activeWidth = 0;  // BVH width of the last mesh render (hipptActiveBvhWidth)
@@ -263,6 +265,11 @@ void destroy_all() {
     State &s = S();
     for (auto &c : s.ctxs) destroy_ctx(c);
     s.ctxs.clear();
+    for (auto &t : s.rngTables) {
+        (void)hipSetDevice(t.first);
+        (void)hipFree(t.second);
+    }
+    s.rngTables.clear();
     if (s.host) (void)hipHostFree(s.host);
     s.host = nullptr;
     s.hostCount = 0;
@@ -419,6 +426,27 @@ bool ensure_spill(Ctx &c, hippt::MeshParams &p, long long blocks, bool spills, i
         c.spillBytes = bytes;
     }
     p.spill = c.spill;
+    return true;
+}
+
+// The memoized random_in_unit_sphere table of c's device (hippt_device.h launch_rng_table),
+// built once per device on first use (16 GiB, a few ms) and shared by the device's contexts.
+bool rng_table(Ctx &c, const uint32_t **out, const char **err) {
+    State &s = S();
+    for (auto &t : s.rngTables)
+        if (t.first == c.device) {
+            *out = t.second;
+            return true;
+        }
+    uint32_t *t = nullptr;
+    HIP_TRY(hipMalloc(&t, hippt::kRngTableBytes));
+    const hipError_t e = hippt::launch_rng_table(t, c.stream);
+    if (e != hipSuccess || hipStreamSynchronize(c.stream) != hipSuccess) {
+        (void)hipFree(t);
+        return fail(err, std::string("rng table: ") + hipGetErrorString(e));
+    }
+    s.rngTables.emplace_back(c.device, t);
+    *out = t;
     return true;
 }
 
@@ -698,6 +726,8 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.wide = quant ? 2 : wide ? 1 : 0;
                         p.stackCap = stackCap;
                         p.topBytes = topBytes;
+                        p.rngTable = nullptr;
+                        if (s.rngTable && !rng_table(c, &p.rngTable, err)) return false;
                         if (s.pathMode == 1) {
                             if (!run_wavefront(c, p, cnt, spills, s.scene.stackBound4 + 3, err)) return false;
                         } else {
@@ -853,7 +883,7 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
     sc.nodes.assign(bvh.nodes.size() / 4, float4{});
     std::memcpy(sc.nodes.data(), bvh.nodes.data(), bvh.nodes.size() * sizeof(uint32_t));
     hippt::Bvh4 bvh4;
-    hippt::collapse_bvh4(bvh, bvh4);
+    hippt::collapse_bvh4(bvh, bvh4, s.bvh);
     hippt::order_bvh4_top(bvh4, kTopOrderNodes);
     sc.nodes4.assign(bvh4.nodes.size() / 4, float4{});
     std::memcpy(sc.nodes4.data(), bvh4.nodes.data(), bvh4.nodes.size() * sizeof(uint32_t));
@@ -1256,6 +1286,22 @@ extern "C" bool hipptSetOption(int key, long long value) {
         if (value < -1 || value > kTopOrderNodes) return false;
         s.ldsTopNodes = int(value);
         return true;
+    case HIPPT_OPT_BVH_COLLAPSE:
+        if (value != 0 && value != 1) return false;
+        s.bvh.collapse = int(value);
+        return true;
+    case HIPPT_OPT_BVH_NODE_COST:
+        if (value < 1 || value > 100000) return false;
+        s.bvh.nodeCost = float(value) / 100.0f;
+        return true;
+    case HIPPT_OPT_BVH_LEAF4:
+        if (value < 1 || value > 15) return false;
+        s.bvh.maxLeaf4 = int(value);
+        return true;
+    case HIPPT_OPT_RNG_TABLE:
+        if (value != 0 && value != 1) return false;
+        s.rngTable = value == 1;
+        return true;
     default: return false;
     }
 }
@@ -1288,6 +1334,10 @@ extern "C" long long hipptGetOption(int key) {
     case HIPPT_OPT_STACK_CAP: return s.stackCap;
     case HIPPT_OPT_BVH_QUANT: return s.bvhQuant;
     case HIPPT_OPT_LDS_TOP_NODES: return s.ldsTopNodes;
+    case HIPPT_OPT_BVH_COLLAPSE: return s.bvh.collapse;
+    case HIPPT_OPT_BVH_NODE_COST: return (long long)std::lround(s.bvh.nodeCost * 100.0f);
+    case HIPPT_OPT_BVH_LEAF4: return s.bvh.maxLeaf4;
+    case HIPPT_OPT_RNG_TABLE: return s.rngTable ? 1 : 0;
     case HIPPT_INFO_LDS_TOP_BYTES: return s.activeTopBytes;
     case HIPPT_INFO_BLOCKS_PER_CU: return s.activeBlocksPerCu;
     default: return -1;
@@ -1311,7 +1361,7 @@ extern "C" hipptBvh *hipptBvhBuild(const float *verts, int numTris, float extent
         fail(err, msg.empty() ? "null vertex pointer" : msg);
         return nullptr;
     }
-    hippt::collapse_bvh4(b->bvh, b->bvh4);
+    hippt::collapse_bvh4(b->bvh, b->bvh4, params);
     hippt::order_bvh4_top(b->bvh4, kTopOrderNodes);
     hippt::quantize_bvh4(b->bvh4, b->bvh4q);
     return b;

@@ -62,6 +62,9 @@ struct MeshParams {
     // 4-wide trees in global memory: bytes of the node array's prefix (the top of the tree,
     // breadth-first, bvh_builder.h order_bvh4_top) copied to LDS address 0 and read from there
     unsigned topBytes;
+    // random_in_unit_sphere memoized (null: the rejection loop): entry 2^32-word table, see
+    // launch_rng_table
+    const uint32_t *rngTable;
 };
 
 // Running average + tonemap over a batch of per-sample radiances
@@ -90,6 +93,11 @@ inline hipError_t check_lds_at_zero(const void *kernel) {
 hipError_t launch_sphere4(const Sphere4Params &p, hipStream_t s);
 hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hipStream_t s);
 hipError_t launch_combine(const CombineParams &p, hipStream_t s);
+// random_in_unit_sphere's rejection loop (RayTracer.h:155-161 with the hash RNG and the short-cycle
+// escape) is a pure function of the RNG state it starts from: table[s] = the state from which the
+// accepted candidate's three draws are made.  One 32-bit word per state: 16 GiB.
+constexpr size_t kRngTableBytes = size_t(4) << 32;
+hipError_t launch_rng_table(uint32_t *table, hipStream_t s);
 // Resident mesh-kernel blocks per CU for a given LDS stack depth and LDS scene size.
 int mesh_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,
                        int ldsTris, bool spill, unsigned topBytes = 0);

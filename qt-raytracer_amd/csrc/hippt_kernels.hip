@@ -300,7 +300,8 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                 finished = true;
             } else if (++depth >= P.maxDepth) {
                 finished = true;  // depth exhausted: contributes 0 (RayTracer.h:582-583)
-            } else if (scatter<FULL, STATS>(r, T.bestT, T.bestI, shade, tris, P.mats, rng, tr, tg, tb, pc)) {
+            } else if (scatter<FULL, STATS>(r, T.bestT, T.bestI, shade, tris, P.mats, rng, tr, tg, tb, pc,
+                                            P.rngTable)) {
                 prepare(r);
                 begin(T);
             } else {
@@ -364,7 +365,33 @@ __global__ __launch_bounds__(256) void combine_kernel(CombineParams P) {
     }
 }
 
+// table[s] for s = 0 .. 2^32-1: the state from which random_in_unit_sphere, entered with state s,
+// draws the candidate it accepts (the loop of trace::rius, escape included).
+__global__ __launch_bounds__(256) void rng_table_kernel(uint32_t *table, uint32_t base) {
+    const uint32_t s0 = base + blockIdx.x * 256u + threadIdx.x;
+    uint32_t s = s0;
+    for (unsigned tries = 1;; ++tries) {
+        const uint32_t from = s;
+        const float x = rand_pm1(s), y = rand_pm1(s), z = rand_pm1(s);
+        if (fmaf(x, x, fmaf(y, y, z * z)) < 1.0f) {
+            table[s0] = from;
+            return;
+        }
+        escape_cycle(s, tries);
+    }
+}
+
 }  // namespace
+
+hipError_t launch_rng_table(uint32_t *table, hipStream_t s) {
+    // a grid dimension holds fewer than 2^32 work-items: 4 launches of 2^30 states
+    for (uint32_t q = 0; q < 4; ++q) {
+        hipLaunchKernelGGL(rng_table_kernel, dim3(1u << 22), dim3(256), 0, s, table, q << 30);
+        const hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
 
 #ifdef HIPPT_DEBUG_TIMELINE
 extern "C" int hipptDebugTimeline(unsigned long long *out, int maxWaves) {

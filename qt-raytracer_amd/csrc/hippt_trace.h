@@ -260,9 +260,24 @@ __device__ __forceinline__ void sky(const Ray &r, float tr, float tg, float tb, 
     L2 = tb * fmaf(al, 1.0f, bl);
 }
 
-// random_in_unit_sphere (RayTracer.h:155-161; x, y, z drawn in that order).
+// random_in_unit_sphere (RayTracer.h:155-161; x, y, z drawn in that order).  With `table`
+// (launch_rng_table) the rejection loop is one lookup: the state the accepted candidate is
+// drawn from, then its three draws — the same draws, hence the same bits, without the loop
+// whose SIMD tail (a wave loops until its unluckiest lane accepts) runs at 19% lane utilization.
+// Measured (r2zd): Cornell -3%, blob70k -18%, random_scene -8%, cornell_mixed +8% — the random
+// 4-byte reads over 16 GiB cost more than the loop's tail; loading the entry when the segment's
+// ray starts (latency behind the traversal) was worse still (Cornell -15%).  Off by default.
 template <bool STATS>
-__device__ __forceinline__ float rius(uint32_t &rng, float &rx, float &ry, float &rz, unsigned *pc) {
+__device__ __forceinline__ float rius(uint32_t &rng, float &rx, float &ry, float &rz, unsigned *pc,
+                                      const uint32_t *table = nullptr) {
+    if (table) {
+        prof<STATS>(pc, 7);
+        rng = table[rng];
+        rx = rand_pm1(rng);
+        ry = rand_pm1(rng);
+        rz = rand_pm1(rng);
+        return fmaf(rx, rx, fmaf(ry, ry, rz * rz));
+    }
     float r2;
     for (unsigned tries = 1;; ++tries) {
         prof<STATS>(pc, 7);
@@ -283,7 +298,7 @@ __device__ __forceinline__ float rius(uint32_t &rng, float &rx, float &ry, float
 template <bool FULL, bool STATS>
 __device__ __forceinline__ bool scatter(Ray &r, float t, int prim, const float4 *shade, const float4 *prims,
                                         const float4 *mats, uint32_t &rng, float &tr, float &tg, float &tb,
-                                        unsigned *pc) {
+                                        unsigned *pc, const uint32_t *rngTable = nullptr) {
     const float4 sh = shade[prim];
     const int mw = __float_as_int(sh.w);
     const float px = fmaf(t, r.dx, r.ox), py = fmaf(t, r.dy, r.oy), pz = fmaf(t, r.dz, r.oz);  // Ray::at
@@ -310,7 +325,7 @@ __device__ __forceinline__ bool scatter(Ray &r, float t, int prim, const float4 
         const float ux = r.dx * il, uy = r.dy * il, uz = r.dz * il;
         const float k = 2.0f * fdot(ux, uy, uz, nx, ny, nz);  // reflect, :174-176
         float qx, qy, qz;
-        rius<STATS>(rng, qx, qy, qz, pc);
+        rius<STATS>(rng, qx, qy, qz, pc, rngTable);
         sx = (ux - k * nx) + fuzz * qx;
         sy = (uy - k * ny) + fuzz * qy;
         sz = (uz - k * nz) + fuzz * qz;
@@ -346,7 +361,7 @@ __device__ __forceinline__ bool scatter(Ray &r, float t, int prim, const float4 
         }
     } else {  // Lambertian::scatter, :477-484: n + unit(random_in_unit_sphere), 1e-8 fallback
         float qx, qy, qz;
-        const float r2 = rius<STATS>(rng, qx, qy, qz, pc);
+        const float r2 = rius<STATS>(rng, qx, qy, qz, pc, rngTable);
         const float inv = 1.0f / sqrtf(r2);  // unit_vector = (1/len)*v, :137-139,151-153
         sx = nx + qx * inv;
         sy = ny + qy * inv;

@@ -238,7 +238,8 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(WfParams W, int cur) {
             finished = true;
         } else if (++q.depth >= P.maxDepth) {
             finished = true;
-        } else if (scatter<FULL, false>(q.r, h.x, tri, P.shade, P.tris, P.mats, q.rng, q.tr, q.tg, q.tb, nullptr)) {
+        } else if (scatter<FULL, false>(q.r, h.x, tri, P.shade, P.tris, P.mats, q.rng, q.tr, q.tg, q.tb, nullptr,
+                                        P.rngTable)) {
             store_slot(W, slot, q);
             again = true;
         } else {

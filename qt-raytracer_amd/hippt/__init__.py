@@ -45,6 +45,10 @@ OPT_BVH_WIDTH = 17
 OPT_STACK_CAP = 18
 OPT_BVH_QUANT = 19
 OPT_LDS_TOP_NODES = 20
+OPT_BVH_COLLAPSE = 21
+OPT_BVH_NODE_COST = 22
+OPT_BVH_LEAF4 = 23
+OPT_RNG_TABLE = 24
 INFO_LDS_TOP_BYTES = 100
 INFO_BLOCKS_PER_CU = 101
 

@@ -153,6 +153,48 @@ def test_bvh4_collapse_keeps_leaves_and_bounds_subtrees(name):
     assert bound == bvh.stack_bound4 and depth == bvh.depth4
 
 
+@pytest.mark.parametrize("name", ["cornell34", "blob70k", "cloud"])
+@pytest.mark.parametrize("leaf4", [4, 8, 15])
+def test_bvh4_sah_collapse_partitions_primitives(name, leaf4):
+    """The SAH-optimal collapse (HIPPT_OPT_BVH_COLLAPSE 1): every primitive lies in exactly one
+    4-wide leaf of at most `leaf4` primitives (2-wide subtrees merged into one leaf are
+    contiguous ranges), every child box contains its leaf's primitives and its child node's
+    boxes, nodes have 2-4 children, and the reported stack bound and depth are the tree's."""
+    sc = {"cloud": scenes.cloud_scene}.get(name, lambda: scenes.get_scene(name))()
+    lib = hippt.load_library()
+    try:
+        assert lib.hipptSetOption(hippt.OPT_BVH_COLLAPSE, 1) and lib.hipptSetOption(hippt.OPT_BVH_LEAF4, leaf4)
+        bvh = hippt.Bvh(sc.verts, extent_hint=800.0)
+    finally:
+        lib.hipptSetOption(hippt.OPT_BVH_COLLAPSE, 0)
+        lib.hipptSetOption(hippt.OPT_BVH_LEAF4, 4)
+    f, kids = _decode4(bvh.nodes4)
+    covered = np.zeros(sc.num_tris, np.int32)
+    bound, depth = 0, 0
+    stack = [(0, 0, 1)]
+    while stack:
+        n, pushes, d = stack.pop()
+        depth = max(depth, d)
+        used = [c for c in range(4) if not (kids[n, c] == -1 and f[n, 0, 0, c] > 1e37)]
+        assert 2 <= len(used) <= 4
+        bound = max(bound, pushes + len(used) - 1)
+        for c in used:
+            k = int(kids[n, c])
+            lo, hi = f[n, :, 0, c], f[n, :, 1, c]
+            if k >= 0:
+                cu = [cc for cc in range(4) if not (kids[k, cc] == -1 and f[k, 0, 0, cc] > 1e37)]
+                assert np.all(f[k, :, 0, cu].T >= lo[:, None] - 1e-3) and np.all(f[k, :, 1, cu].T <= hi[:, None] + 1e-3)
+                stack.append((k, pushes + len(used) - 1, d + 1))
+            else:
+                first, count = (~k) >> 4, (~k) & 15
+                assert count <= max(leaf4, 4)
+                covered[first:first + count] += 1
+                v = sc.verts[bvh.order[first:first + count]].reshape(-1, 3)
+                assert np.all(v >= lo) and np.all(v <= hi)
+    assert np.all(covered == 1)
+    assert bound == bvh.stack_bound4 and depth == bvh.depth4
+
+
 @pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene", "cornell_mixed", "voxel", "cloud"])
 def test_bvh4_quantized_boxes_contain_float_boxes(name):
     """quantize_bvh4 (hipptBvh4QCopy): every child box decoded exactly (origin + byte * scale, a

@@ -27,7 +27,9 @@ def pt():
                  (hippt.OPT_COUNT_TRAVERSAL, 0), (hippt.OPT_BLOCKS_PER_CU, 0), (hippt.OPT_LDS_SCENE, 1),
                  (hippt.OPT_PATH_MODE, 0), (hippt.OPT_WAVEFRONT_SLOTS, 1 << 24), (hippt.OPT_LEAF_EXIT, -1),
                  (hippt.OPT_NODE_EXIT, -1), (hippt.OPT_BVH_SAH, 1), (hippt.OPT_BVH_WIDTH, 0),
-                 (hippt.OPT_STACK_CAP, 0), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_LDS_TOP_NODES, -1)):
+                 (hippt.OPT_STACK_CAP, 0), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_LDS_TOP_NODES, -1),
+                 (hippt.OPT_RNG_TABLE, 0), (hippt.OPT_BVH_COLLAPSE, 0), (hippt.OPT_BVH_NODE_COST, 200),
+                 (hippt.OPT_BVH_LEAF4, 4)):
         t.setOption(k, v)
     t.resetStats()
     yield t
@@ -345,6 +347,29 @@ def test_lds_top_of_tree_does_not_change_results(pt, name):
                     if top == 0:
                         assert top_bytes == 0
                 pt.setOption(hippt.OPT_COUNT_TRAVERSAL, 0)
+
+
+@pytest.mark.parametrize("name", ["cornell34", "cornell_mixed", "random_scene", "blob70k"])
+def test_rng_table_and_sah_collapse_do_not_change_results(pt, name):
+    """The memoized random_in_unit_sphere (HIPPT_OPT_RNG_TABLE 1: one lookup per Lambertian or
+    Metal scatter instead of the rejection loop) and the loop (the default) give the oracle's
+    image bit for bit, megakernel and wavefront; so does the SAH-optimal 4-wide collapse
+    (HIPPT_OPT_BVH_COLLAPSE 1, leaves merged up to 8 primitives)."""
+    sc = scenes.get_scene(name)
+    w, h = (40, 24) if name == "random_scene" else (48, 32)
+    ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
+    for collapse in (0, 1):
+        pt.setOption(hippt.OPT_BVH_COLLAPSE, collapse)
+        pt.setOption(hippt.OPT_BVH_LEAF4, 8)
+        pt.uploadMesh(sc)
+        for mode in (0, 1):
+            pt.setOption(hippt.OPT_PATH_MODE, mode)
+            for tab in (1, 0):
+                pt.setOption(hippt.OPT_RNG_TABLE, tab)
+                assert pt.initialize(w, h)
+                assert pt.renderFrames(3, 8)
+                got = pt.readback()
+                _assert_same(got[0], got[1], ora[0], ora[1])
 
 
 @pytest.mark.parametrize("mode", [0, 1])

@@ -20,7 +20,8 @@ from hippt import scenes  # noqa: E402
 KEYS = {"wave": hippt.OPT_WAVE_THRESHOLD, "chunk": hippt.OPT_CHUNK, "lds": hippt.OPT_LDS_SCENE,
         "width": hippt.OPT_BVH_WIDTH, "stackcap": hippt.OPT_STACK_CAP, "leafexit": hippt.OPT_LEAF_EXIT,
         "nodeexit": hippt.OPT_NODE_EXIT, "quant": hippt.OPT_BVH_QUANT,
-        "top": hippt.OPT_LDS_TOP_NODES}
+        "top": hippt.OPT_LDS_TOP_NODES, "collapse": hippt.OPT_BVH_COLLAPSE,
+        "ncost": hippt.OPT_BVH_NODE_COST}
 
 
 def main():

@@ -27,8 +27,10 @@ KEYS = {"wave": hippt.OPT_WAVE_THRESHOLD, "chunk": hippt.OPT_CHUNK, "scratch": h
         "depth": hippt.OPT_BVH_MAX_DEPTH, "leafexit": hippt.OPT_LEAF_EXIT,
         "nodeexit": hippt.OPT_NODE_EXIT, "sah": hippt.OPT_BVH_SAH,
         "width": hippt.OPT_BVH_WIDTH, "stackcap": hippt.OPT_STACK_CAP,
-        "quant": hippt.OPT_BVH_QUANT, "top": hippt.OPT_LDS_TOP_NODES}
-REUPLOAD = {"leaf", "tcost", "depth", "sah"}  # build parameters: take effect at the next upload
+        "quant": hippt.OPT_BVH_QUANT, "top": hippt.OPT_LDS_TOP_NODES,
+        "collapse": hippt.OPT_BVH_COLLAPSE, "ncost": hippt.OPT_BVH_NODE_COST, "leaf4": hippt.OPT_BVH_LEAF4,
+        "rngtab": hippt.OPT_RNG_TABLE}
+REUPLOAD = {"leaf", "tcost", "depth", "sah", "collapse", "ncost", "leaf4"}  # build parameters: take effect at the next upload
 
 
 def main():
