@@ -620,7 +620,8 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 s.activeWidth = wide ? 4 : 2;
                 const int numNodes = wide ? s.scene.numNodes4 : s.scene.numNodes, numTris = s.scene.numTris;
                 // small scenes live in LDS (scene bytes beyond the stack under the limit)
-                const bool ldsScene = s.ldsScene && hippt::mesh_lds_bytes(0, numNodes, numTris, wide) <=
+                const int numMats = int(s.scene.mats.size() / 2);
+                const bool ldsScene = s.ldsScene && hippt::mesh_lds_bytes(0, numNodes, numTris, wide, 0, numMats) <=
                                                         hippt::mesh_lds_scene_limit();
                 // LDS stack entries per lane: 2-wide = interior levels (+1 spare); 4-wide = the
                 // builder's exact bound up to kWideStackCap (+3 spare; deeper stacks spill their
@@ -665,11 +666,11 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                     occupancy_key(s.scene.version, stackDepth, ldsScene, s.scene.full, wide, quant, spills) ^
                     ((long long)topBytes << 40);
                 if (c.occKey != occKey) {
-                    const int ln = ldsScene ? numNodes : 0, lt = ldsScene ? numTris : 0;
+                    const int ln = ldsScene ? numNodes : 0, lt = ldsScene ? numTris : 0, lm = ldsScene ? numMats : 0;
                     c.meshBlocksPerCu[0] = hippt::mesh_blocks_per_cu(false, s.scene.full, wide, quant, stackDepth,
-                                                                     ln, lt, spills, topBytes);
+                                                                     ln, lt, spills, topBytes, lm);
                     c.meshBlocksPerCu[1] = hippt::mesh_blocks_per_cu(true, s.scene.full, wide, quant, stackDepth,
-                                                                     ln, lt, spills, topBytes);
+                                                                     ln, lt, spills, topBytes, lm);
                     c.occKey = occKey;
                 }
                 s.activeTopBytes = topBytes;
@@ -708,6 +709,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.stackDepth = stackDepth;
                         p.numNodes = numNodes;
                         p.numTris = numTris;
+                        p.numMats = numMats;
                         p.ldsScene = ldsScene ? 1 : 0;
                         p.full = s.scene.full ? 1 : 0;
                         // shade once fewer than this many lanes still traverse: LDS scenes' short node

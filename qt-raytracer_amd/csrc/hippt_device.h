@@ -45,7 +45,7 @@ struct MeshParams {
     unsigned bandPixels, totalItems;
     float rcpBandPixels, rcpWidth;  // 1/bandPixels, 1/width for the item -> (frame, x, y) split
     int stackDepth;        // LDS stack entries per lane (>= BVH interior levels)
-    int numNodes, numTris;
+    int numNodes, numTris, numMats;
     int ldsScene;          // 1: copy nodes/triangles/shading into LDS (small scenes)
     int full;              // 1: spheres or non-Lambertian materials present (general kernel)
     int waveThreshold;     // shade once fewer than this many lanes still traverse
@@ -100,8 +100,8 @@ constexpr size_t kRngTableBytes = size_t(4) << 32;
 hipError_t launch_rng_table(uint32_t *table, hipStream_t s);
 // Resident mesh-kernel blocks per CU for a given LDS stack depth and LDS scene size.
 int mesh_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,
-                       int ldsTris, bool spill, unsigned topBytes = 0);
-size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide, unsigned topBytes = 0);
+                       int ldsTris, bool spill, unsigned topBytes = 0, int ldsMats = 0);
+size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide, unsigned topBytes = 0, int ldsMats = 0);
 // LDS bytes per block that keep the persistent grid's resident blocks within a CU's LDS
 size_t mesh_lds_block_budget();
 size_t mesh_lds_scene_limit();

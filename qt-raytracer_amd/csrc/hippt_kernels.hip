@@ -208,11 +208,15 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     int *const stk = LDS_SCENE ? lds + P.numNodes * ldsNodeF4 * 4 : lds + (TOP ? (P.topBytes >> 2) : 0u);
     int *const my = stk + threadIdx.x;
 
-    const float4 *nodes = P.nodes, *tris = P.tris, *shade = P.shade;
+    const float4 *nodes = P.nodes, *tris = P.tris, *shade = P.shade, *mats = P.mats;
     if (LDS_SCENE) {
         float4 *sNodes = reinterpret_cast<float4 *>(lds);
         float4 *sTris = reinterpret_cast<float4 *>(stk + (P.stackDepth + 1) * kMeshBlock);
         float4 *sShade = sTris + P.numTris * 3;
+        // the materials too: a shading step's shade-record -> material chain then stays in LDS
+        float4 *sMats = sShade + P.numTris;
+        for (int i = threadIdx.x; i < P.numMats * 2; i += kMeshBlock) sMats[i] = P.mats[i];
+        mats = sMats;
         if (WIDE) {
             for (int i = threadIdx.x; i < P.numNodes * kLdsNode4F4; i += kMeshBlock) sNodes[i] = P.nodes[i];
         } else {
@@ -300,7 +304,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                 finished = true;
             } else if (++depth >= P.maxDepth) {
                 finished = true;  // depth exhausted: contributes 0 (RayTracer.h:582-583)
-            } else if (scatter<FULL, STATS>(r, T.bestT, T.bestI, shade, tris, P.mats, rng, tr, tg, tb, pc,
+            } else if (scatter<FULL, STATS>(r, T.bestT, T.bestI, shade, tris, mats, rng, tr, tg, tb, pc,
                                             P.rngTable)) {
                 prepare(r);
                 begin(T);
@@ -412,9 +416,10 @@ hipError_t launch_sphere4(const Sphere4Params &p, hipStream_t s) {
 
 // Stack: one spare slot per lane above the deepest level for the speculative far-child
 // write; then (LDS_SCENE) the scene copy.
-size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide, unsigned topBytes) {
+size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide, unsigned topBytes, int ldsMats) {
     return size_t(stackDepth + 1) * kMeshBlock * sizeof(int) +
-           size_t(ldsNodes) * (wide ? kLdsNode4F4 : kLdsNodeF4) * 16 + size_t(ldsTris) * (3 + 1) * 16 + topBytes;
+           size_t(ldsNodes) * (wide ? kLdsNode4F4 : kLdsNodeF4) * 16 + size_t(ldsTris) * (3 + 1) * 16 + topBytes +
+           size_t(ldsMats) * 2 * 16;
 }
 
 size_t mesh_lds_scene_limit() { return 24u << 10; }
@@ -453,7 +458,8 @@ hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hip
     const bool lds = p.ldsScene != 0;
     if (p.topBytes && (lds || !p.wide || p.topBytes % (p.wide == 2 ? 64u : 128u) || p.topBytes > (unsigned(p.numNodes) << (p.wide == 2 ? 6 : 7))))
         return hipErrorInvalidValue;
-    const size_t bytes = mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0, p.wide != 0, p.topBytes);
+    const size_t bytes =
+        mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0, p.wide != 0, p.topBytes, lds ? p.numMats : 0);
     const MeshFn fn = mesh_fn(countTraversal, lds, p.full != 0, p.wide != 0, p.wide == 2 && !lds, p.spill != nullptr);
     if (p.wide && (lds || p.topBytes)) {
         const hipError_t e = check_lds_at_zero(reinterpret_cast<const void *>(fn));
@@ -474,10 +480,10 @@ hipError_t launch_combine(const CombineParams &p, hipStream_t s) {
 }
 
 int mesh_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,
-                       int ldsTris, bool spill, unsigned topBytes) {
+                       int ldsTris, bool spill, unsigned topBytes, int ldsMats) {
     int n = 0;
     const bool lds = ldsNodes > 0;
-    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, wide, topBytes);
+    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, wide, topBytes, ldsMats);
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
         &n, mesh_fn(countTraversal, lds, full, wide, quant && wide && !lds, spill), kMeshBlock, bytes);
     if (e != hipSuccess || n <= 0) n = 1;
