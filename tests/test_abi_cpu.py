@@ -80,6 +80,39 @@ def test_options_validate():
     assert not lib.hipptSetOption(hippt.OPT_WAVE_THRESHOLD, -2)
 
 
+@pytest.mark.parametrize("key,good,bad,default", [
+    (hippt.OPT_LDS_TOP_NODES, (0, 1, 85, 1365), (-2, 1366), -1),
+    (hippt.OPT_BVH_COLLAPSE, (0, 1), (-1, 2), 0),
+    (hippt.OPT_BVH_NODE_COST, (1, 250, 100000), (0, 100001), 200),
+    (hippt.OPT_BVH_LEAF4, (1, 8, 15), (0, 16), 4),
+    (hippt.OPT_RNG_TABLE, (0, 1), (-1, 2), 0),
+    (hippt.OPT_STACK_CAP, (0, 4, 30), (3, 31), 0),
+    (hippt.OPT_BVH_QUANT, (-1, 0, 1), (-2, 2), -1),
+])
+def test_round2_options_round_trip(key, good, bad, default):
+    """Each option accepts its documented range (include/hippt.h), reads back what was set,
+    rejects values outside it without changing the setting, and starts at its default."""
+    lib = hippt.load_library()
+    assert lib.hipptGetOption(key) == default
+    try:
+        for v in good:
+            assert lib.hipptSetOption(key, v), v
+            assert lib.hipptGetOption(key) == v
+        for v in bad:
+            assert not lib.hipptSetOption(key, v), v
+            assert lib.hipptGetOption(key) == good[-1]
+    finally:
+        assert lib.hipptSetOption(key, default)
+
+
+def test_info_keys_before_any_render():
+    """The read-only facts of the last megakernel render are 0 before one ran."""
+    lib = hippt.load_library()
+    assert lib.hipptGetOption(hippt.INFO_LDS_TOP_BYTES) >= 0
+    assert lib.hipptGetOption(hippt.INFO_BLOCKS_PER_CU) >= 0
+    assert not lib.hipptSetOption(hippt.INFO_LDS_TOP_BYTES, 1)
+
+
 def test_mesh_upload_validates_inputs():
     pt = hippt.PathTracer()
     sc = scenes.cornell34()
