@@ -218,7 +218,18 @@ enum {
     , HIPPT_OPT_RNG_TABLE = 24      /* 1: random_in_unit_sphere's rejection loop as one lookup in a 16 GiB
                                        per-device table of its outcome for every 32-bit RNG state (built on
                                        first use); 0 (default): the loop.  Same results either way */
+    , HIPPT_OPT_PIXEL_FORMAT = 25   /* output frame words of the hipptRenderFrames* calls: HIPPT_PIXEL_ARGB
+                                       (default, the CUDA backend's) or HIPPT_PIXEL_RGBA8 (the GL / Vulkan
+                                       backends'); cudaPathTracerRender always writes ARGB */
 };
+/* Output frame word formats (HIPPT_OPT_PIXEL_FORMAT).  Both map an accumulated colour c to
+ * sqrt(clamp(c, 0, 1)) per channel.
+ *   ARGB:  0xAARRGGBB, channel = uint(x * 255) truncated (CudaPathTracerKernel.cu:171-178).
+ *   RGBA8: bytes R, G, B, A in memory (0xAABBGGRR), channel = x * 255 rounded to nearest, ties to
+ *          even: the RGBA8 UNORM texel the GL (GpuPathTracer.cpp:284-285, GL_RGBA8 image) and
+ *          Vulkan (pathtrace_vulkan.comp:113-114, VK_FORMAT_R8G8B8A8_UNORM, copied to
+ *          VulkanPathTracer::hostPixels) backends store. */
+enum { HIPPT_PIXEL_ARGB = 0, HIPPT_PIXEL_RGBA8 = 1 };
 /* Read-only (hipptGetOption) facts of the last megakernel render: LDS bytes of the top of the tree,
  * persistent-grid blocks per CU. */
 enum { HIPPT_INFO_LDS_TOP_BYTES = 100, HIPPT_INFO_BLOCKS_PER_CU = 101 };

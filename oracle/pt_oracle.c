@@ -263,6 +263,20 @@ static inline unsigned q8(float c) {
     return (unsigned)(sqrtf(fminf(fmaxf(c, 0.0f), 1.0f)) * 255.0f);
 }
 
+/* The GL / Vulkan backends' RGBA8 UNORM texel of the same colour (GpuPathTracer.cpp:284-285,
+ * pathtrace_vulkan.comp:113-114): bytes R, G, B, A, channel = sqrt(clamp(c, 0, 1)) * 255
+ * rounded to nearest, ties to even (the float-to-UNORM conversion, round to nearest). */
+static inline unsigned u8n(float c) {
+    return (unsigned)rintf(sqrtf(fminf(fmaxf(c, 0.0f), 1.0f)) * 255.0f);
+}
+
+void po_rgba8(const float *acc4, long long n, uint32_t *out) {
+    for (long long i = 0; i < n; ++i) {
+        const float *a = acc4 + 4 * i;
+        out[i] = (255u << 24) | (u8n(a[2]) << 16) | (u8n(a[1]) << 8) | u8n(a[0]);
+    }
+}
+
 uint32_t po_accumulate(float acc[4], const float s[3], int f) {
     float ff = (float)f, fc = (float)(f + 1);
     acc[0] = fmaf(acc[0], ff, s[0]) / fc;

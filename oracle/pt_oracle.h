@@ -119,6 +119,8 @@ void po_mesh_sample(const po_scene *sc, int width, int height, int x, int y, int
 
 /* Running-average + tonemap step (CudaPathTracerKernel.cu:157-178). */
 uint32_t po_accumulate(float acc[4], const float sample[3], int frame_index);
+/* RGBA8 UNORM words (GL / Vulkan backends) of n accumulated RGBA float colours. */
+void po_rgba8(const float *acc4, long long n, uint32_t *out);
 
 #ifdef __cplusplus
 }

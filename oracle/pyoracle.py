@@ -76,6 +76,7 @@ def lib() -> ctypes.CDLL:
     sig("po_mesh_frames", None, ctypes.c_void_p, i, i, i, i, i, i, i, pf, pu32, pu64, i)
     sig("po_mesh_sample", None, ctypes.c_void_p, i, i, i, i, i, i, pf, pi)
     sig("po_accumulate", u32, pf, pf, i)
+    sig("po_rgba8", None, pf, ctypes.c_longlong, pu32)
     _lib = L
     return L
 
@@ -224,3 +225,12 @@ def closest_hit(scene, o, d, tmin=0.001):
 def argb_to_rgb(img: np.ndarray) -> np.ndarray:
     img = np.asarray(img, np.uint32)
     return np.stack([(img >> 16) & 255, (img >> 8) & 255, img & 255], axis=-1).astype(np.uint8)
+
+
+def rgba8(acc: np.ndarray) -> np.ndarray:
+    """The GL / Vulkan backends' RGBA8 UNORM words (include/hippt.h HIPPT_PIXEL_RGBA8) of an
+    accumulation image (float32 [..., 4]), as the kernels write them with HIPPT_OPT_PIXEL_FORMAT 1."""
+    a = np.ascontiguousarray(acc, dtype=np.float32)
+    out = np.zeros(a.shape[:-1], np.uint32)
+    lib().po_rgba8(_p(a, ctypes.c_float), a.size // 4, _p(out, ctypes.c_uint32))
+    return out

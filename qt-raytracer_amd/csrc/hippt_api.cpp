@@ -135,6 +135,7 @@ struct State {
     int bvhQuant = -1;  // 4-wide global-memory traversal over 8-bit child boxes (-1: automatic)
     int ldsTopNodes = -1;  // top-of-tree nodes copied into LDS for global-memory trees (-1: automatic)
     bool rngTable = false;  // memoized random_in_unit_sphere (HIPPT_OPT_RNG_TABLE)
+    int pixelFormat = HIPPT_PIXEL_ARGB;  // output frame words (HIPPT_OPT_PIXEL_FORMAT)
     std::vector<std::pair<int, uint32_t *>> rngTables;  // per device, built on first use
     unsigned activeTopBytes = 0;  // of the last mesh render (hipptGetOption HIPPT_INFO_*)
     int activeBlocksPerCu = 0;
@@ -586,7 +587,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
         if (rows > 0 && count > 0) {
             if (!mesh) {
                 hippt::Sphere4Params p{c.accum, c.out, c.stats, s.width, s.height, c.y0, rows, c.stride, firstFrame, count,
-                                       maxDepth};
+                                       maxDepth, s.pixelFormat};
                 EventPair ev;
                 if (!next_events(c, ev, err)) return false;
                 HIP_TRY(hipEventRecord(ev.a, c.stream));
@@ -746,7 +747,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                             c.pending.push_back({0, ev});
                         }
                     }
-                    hippt::CombineParams q{c.accum, c.out, c.scratch, bandPixels, total, firstFrame + b, nf};
+                    hippt::CombineParams q{c.accum, c.out, c.scratch, bandPixels, total, firstFrame + b, nf, s.pixelFormat};
                     EventPair ev2;
                     if (!next_events(c, ev2, err)) return false;
                     HIP_TRY(hipEventRecord(ev2.a, c.stream));
@@ -793,7 +794,14 @@ extern "C" bool cudaPathTracerInit(int width, int height, const char **errorMess
 extern "C" bool cudaPathTracerRender(int frameIndex, int maxDepth, const unsigned int **hostPixels,
                                      const char **errorMessage) {
     std::lock_guard<std::mutex> g(S().mu);
-    return render_locked(frameIndex, 1, maxDepth, hostPixels, errorMessage);
+    // the CUDA backend's ABI always hands out its ARGB words (HIPPT_OPT_PIXEL_FORMAT applies to
+    // the hippt* render calls)
+    State &s = S();
+    const int format = s.pixelFormat;
+    s.pixelFormat = HIPPT_PIXEL_ARGB;
+    const bool ok = render_locked(frameIndex, 1, maxDepth, hostPixels, errorMessage);
+    s.pixelFormat = format;
+    return ok;
 }
 
 extern "C" void cudaPathTracerShutdown(void) {
@@ -1304,6 +1312,10 @@ extern "C" bool hipptSetOption(int key, long long value) {
         if (value != 0 && value != 1) return false;
         s.rngTable = value == 1;
         return true;
+    case HIPPT_OPT_PIXEL_FORMAT:
+        if (value != HIPPT_PIXEL_ARGB && value != HIPPT_PIXEL_RGBA8) return false;
+        s.pixelFormat = int(value);
+        return true;
     default: return false;
     }
 }
@@ -1340,6 +1352,7 @@ extern "C" long long hipptGetOption(int key) {
     case HIPPT_OPT_BVH_NODE_COST: return (long long)std::lround(s.bvh.nodeCost * 100.0f);
     case HIPPT_OPT_BVH_LEAF4: return s.bvh.maxLeaf4;
     case HIPPT_OPT_RNG_TABLE: return s.rngTable ? 1 : 0;
+    case HIPPT_OPT_PIXEL_FORMAT: return s.pixelFormat;
     case HIPPT_INFO_LDS_TOP_BYTES: return s.activeTopBytes;
     case HIPPT_INFO_BLOCKS_PER_CU: return s.activeBlocksPerCu;
     default: return -1;

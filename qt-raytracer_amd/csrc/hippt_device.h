@@ -21,7 +21,11 @@ struct Sphere4Params {
     unsigned long long *stats;
     int width, height, y0, rows, rowStride;  // image rows y0 + k*rowStride, k < rows
     int firstFrame, frames, maxDepth;
+    int format;  // kPixelArgb / kPixelRgba8
 };
+
+// Pixel word formats of the output frame (HIPPT_OPT_PIXEL_FORMAT)
+enum { kPixelArgb = 0, kPixelRgba8 = 1 };
 
 // Mesh megakernel: one persistent grid drains `totalItems` (pixel, frame) samples of the band's
 // rows and frames [firstFrame, firstFrame+frames).
@@ -75,6 +79,7 @@ struct CombineParams {
     const float *scratch;
     unsigned bandPixels, totalItems;
     int firstFrame, frames;
+    int format;  // kPixelArgb / kPixelRgba8
 };
 
 // Material kinds (RayTracer.h:473-540) and the sphere flag of a shading record.

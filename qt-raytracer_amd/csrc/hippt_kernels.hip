@@ -32,6 +32,19 @@ __device__ __forceinline__ unsigned q8(float c) {
     return unsigned(sqrtf(fminf(fmaxf(c, 0.0f), 1.0f)) * 255.0f);
 }
 
+// The displayed pixel of an accumulated colour.  kPixelArgb: the CUDA backend's word
+// (CudaPathTracerKernel.cu:171-178): 0xAARRGGBB, channel = uint(sqrt(clamp(c, 0, 1)) * 255)
+// truncated.  kPixelRgba8: the GL / Vulkan backends' RGBA8 UNORM image texel
+// (GpuPathTracer.cpp:284-285, pathtrace_vulkan.comp:113-114): bytes R, G, B, A in memory
+// (0xAABBGGRR), channel = sqrt(clamp(c, 0, 1)) * 255 rounded to nearest, ties to even.
+__device__ __forceinline__ uint32_t pack_pixel(float r, float g, float b, int format) {
+    if (format == kPixelRgba8) {
+        const auto u8 = [](float c) { return unsigned(rintf(sqrtf(fminf(fmaxf(c, 0.0f), 1.0f)) * 255.0f)); };
+        return (255u << 24) | (u8(b) << 16) | (u8(g) << 8) | u8(r);
+    }
+    return (255u << 24) | (q8(r) << 16) | (q8(g) << 8) | q8(b);
+}
+
 // =========================================================================================
 // Legacy scene: literal restatement of CudaPathTracerKernel.cu:37-179 (no contraction).
 // =========================================================================================
@@ -138,7 +151,7 @@ __global__ __launch_bounds__(256) void sphere4_kernel(Sphere4Params P) {
             acc.y = (acc.y * ff + rad.y) / fc;
             acc.z = (acc.z * ff + rad.z) / fc;
             acc.w = 1.0f;
-            outp = (255u << 24) | (q8(acc.x) << 16) | (q8(acc.y) << 8) | q8(acc.z);
+            outp = pack_pixel(acc.x, acc.y, acc.z, P.format);
         }
         if (P.frames > 0) {
             P.accum[idx] = acc;
@@ -365,7 +378,7 @@ __global__ __launch_bounds__(256) void combine_kernel(CombineParams P) {
         }
         acc.w = 1.0f;
         P.accum[p] = acc;
-        P.out[p] = (255u << 24) | (q8(acc.x) << 16) | (q8(acc.y) << 8) | q8(acc.z);
+        P.out[p] = pack_pixel(acc.x, acc.y, acc.z, P.format);
     }
 }
 

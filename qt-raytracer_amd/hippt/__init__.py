@@ -49,6 +49,9 @@ OPT_BVH_COLLAPSE = 21
 OPT_BVH_NODE_COST = 22
 OPT_BVH_LEAF4 = 23
 OPT_RNG_TABLE = 24
+OPT_PIXEL_FORMAT = 25
+PIXEL_ARGB = 0
+PIXEL_RGBA8 = 1
 INFO_LDS_TOP_BYTES = 100
 INFO_BLOCKS_PER_CU = 101
 

@@ -53,3 +53,35 @@ def test_cpp_host_mesh_file_matches_oracle(tmp_path, mode):
     ora_px, _, segs, samples = po.MeshScene(sc, 80, 48).frames(0, 8, 8)
     assert np.array_equal(px, ora_px)
     assert info["frames"] == 8 and info["pixel_samples"] == samples and info["segments"] == segs
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("backend,extra", [("vulkan", []), ("gl", []), ("gl", ["--per-frame"])])
+@pytest.mark.parametrize("depth,clamped", [(8, 8), (100, 64), (0, 1)])
+def test_cpp_host_vulkan_and_gl_interfaces_match_oracle(tmp_path, backend, extra, depth, clamped):
+    """HipVulkanPathTracer (VulkanPathTracer's interface) and HipGpuPathTracer (GpuPathTracer's)
+    on the reference kernels' 4-sphere scene: RGBA8 UNORM words equal to the oracle's accumulation
+    quantized as the GL / Vulkan image stores it, the bounce count clamped to 1..64 as those
+    backends do (GpuPathTracer.cpp:57, VulkanPathTracer.cpp:95), one frame index per sample."""
+    out = tmp_path / "frame.rgba"
+    info = _run("--backend", backend, "--width", 64, "--height", 40, "--spp", 5, "--depth", depth, "--out", out,
+                *extra)
+    assert info["backend"] == backend and info["frames"] == 5
+    px = np.fromfile(out, np.uint32).reshape(40, 64)
+    _, acc = po.sphere4(64, 40, 0, 5, clamped)
+    assert np.array_equal(px, po.rgba8(acc))
+
+
+@pytest.mark.gpu
+def test_cpp_host_gl_interface_mesh_scene(tmp_path):
+    sc = scenes.cornell34()
+    obj = tmp_path / "cornell.obj"
+    scenes.write_obj(sc, str(obj), style="quads")
+    out = tmp_path / "mesh.rgba"
+    albedo = ";".join(",".join(f"{c:.9g}" for c in a) for a in sc.albedo)
+    info = _run("--backend", "gl", "--mesh", obj, "--albedo", albedo, "--width", 48, "--height", 32, "--spp", 4,
+                "--depth", 8, "--out", out)
+    px = np.fromfile(out, np.uint32).reshape(32, 48)
+    _, acc, segs, samples = po.MeshScene(sc, 48, 32).frames(0, 4, 8)
+    assert np.array_equal(px, po.rgba8(acc))
+    assert info["pixel_samples"] == samples and info["segments"] == segs

@@ -29,7 +29,7 @@ def pt():
                  (hippt.OPT_NODE_EXIT, -1), (hippt.OPT_BVH_SAH, 1), (hippt.OPT_BVH_WIDTH, 0),
                  (hippt.OPT_STACK_CAP, 0), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_LDS_TOP_NODES, -1),
                  (hippt.OPT_RNG_TABLE, 0), (hippt.OPT_BVH_COLLAPSE, 0), (hippt.OPT_BVH_NODE_COST, 200),
-                 (hippt.OPT_BVH_LEAF4, 4)):
+                 (hippt.OPT_BVH_LEAF4, 4), (hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_ARGB)):
         t.setOption(k, v)
     t.resetStats()
     yield t
@@ -370,6 +370,34 @@ def test_rng_table_and_sah_collapse_do_not_change_results(pt, name):
                 assert pt.renderFrames(3, 8)
                 got = pt.readback()
                 _assert_same(got[0], got[1], ora[0], ora[1])
+
+
+@pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene"])
+def test_rgba8_pixel_format(pt, name):
+    """HIPPT_OPT_PIXEL_FORMAT = RGBA8 (the GL / Vulkan backends' image words): the accumulation is
+    unchanged and every word is the oracle's RGBA8 UNORM quantization of it; the reference ABI
+    (cudaPathTracerRender) still hands out ARGB words with the option set."""
+    sc = scenes.get_scene(name)
+    pt.uploadMesh(sc)
+    w, h = (40, 24) if name == "random_scene" else (48, 32)
+    ora_px, ora_acc = po.MeshScene(sc, w, h).frames(0, 3, 8)[:2]
+    pt.setOption(hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_RGBA8)
+    try:
+        for mode in (0, 1):
+            pt.setOption(hippt.OPT_PATH_MODE, mode)
+            assert pt.initialize(w, h)
+            assert pt.renderFrames(3, 8)
+            px, acc = pt.readback()
+            assert acc.tobytes() == ora_acc.tobytes()
+            assert np.array_equal(px, po.rgba8(ora_acc))
+        lib = hippt.load_library()
+        assert lib.cudaPathTracerInit(w, h, None)
+        for f in range(3):
+            assert lib.cudaPathTracerRender(f, 8, None, None)
+        px, acc = pt.readback()
+        assert np.array_equal(px, ora_px) and acc.tobytes() == ora_acc.tobytes()
+    finally:
+        pt.setOption(hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_ARGB)
 
 
 @pytest.mark.parametrize("mode", [0, 1])

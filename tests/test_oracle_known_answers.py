@@ -120,3 +120,19 @@ def test_degenerate_triangle_never_hit():
 def test_tmin_rejects_self_hit():  # ray_color uses t_min = 0.001 (RayTracer.h:585)
     tri = po.tri_setup([-1, -1, -0.0005, 1, -1, -0.0005, 0, 1, -0.0005])
     assert not po.tri_hit(tri, (0, 0, 0), (0, 0, -1))[0]
+
+
+def test_rgba8_quantization_known_answers():
+    """pyoracle.rgba8 (pt_oracle.c po_rgba8): the GL / Vulkan RGBA8 UNORM word of an accumulated
+    colour — sqrt(clamp(c, 0, 1)) * 255 rounded to nearest, ties to even, bytes R, G, B, A —
+    against a numpy float32 restatement, on hand-picked and random colours."""
+    hand = np.array([[0.25, 0.5, 1.0, 1.0], [0.0, -1.0, 2.0, 1.0], [np.nan, 1e-30, 0.999, 1.0]], np.float32)
+    rng = np.random.default_rng(7)
+    acc = np.concatenate([rng.random((4096, 4), dtype=np.float32) * np.float32(1.2) - np.float32(0.1), hand[:2]])
+    c = np.sqrt(np.clip(acc[:, :3], np.float32(0), np.float32(1))) * np.float32(255)
+    q = np.rint(c).astype(np.uint32)
+    want = np.uint32(255 << 24) | (q[:, 2] << 16) | (q[:, 1] << 8) | q[:, 0]
+    assert np.array_equal(po.rgba8(acc), want)
+    assert int(po.rgba8(hand[:1])[0]) == 0xFFFFB480  # 0.5*255 = 127.5 -> 128 (even), 180.3 -> 180
+    assert int(po.rgba8(hand[1:2])[0]) == 0xFFFF0000  # clamped: R 0, G 0, B 255
+    assert int(po.rgba8(hand[2:3])[0]) & 0xFF == 0  # NaN clamps to 0 (fminf/fmaxf)
