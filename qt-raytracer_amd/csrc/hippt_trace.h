@@ -41,6 +41,46 @@ __device__ __forceinline__ float rand_pm1(uint32_t &s) {
     return fmaf(float(s), 0x1p-31f, -1.0f);
 }
 
+// Correctly rounded square root and reciprocal as short sequences (the IEEE expansions hipcc
+// emits for sqrtf and 1.0f/x are 15 and 11 instructions: denormal scaling, class tests,
+// v_div_scale/fmas/fixup).  Both are checked against hipcc's IEEE sqrtf / 1.0f/x on EVERY float
+// bit pattern on gfx950 (tools/micro/rn_check.hip, tests/test_gpu_rounding.py):
+//   sqrt_fix(x) == sqrtf(x)                   for every x except the denormals (x >= 2^-104)
+//   rcp_nr(x)   == 1.0f / x                   for 2^-126 <= |x| < 2^126
+//   rcp_nr(sqrt_fix(x)) == 1.0f / sqrtf(x)    for 2^-105 <= x < +inf
+// v_sqrt_f32 is within one ulp, so the correctly rounded root is s or a neighbour, picked by
+// the signs of the exact residuals x - s'*s (one fma each); v_rcp_f32 is within one ulp and one
+// Newton step rounds correctly.
+__device__ __forceinline__ float sqrt_fix(float x) {
+    const float s = __builtin_amdgcn_sqrtf(x);
+    const float sm = __uint_as_float(__float_as_uint(s) - 1u);
+    const float sp = __uint_as_float(__float_as_uint(s) + 1u);
+    float r = s;
+    if (fmaf(-sm, s, x) <= 0.0f) r = sm;
+    if (fmaf(-sp, s, x) > 0.0f) r = sp;
+    return r;
+}
+
+__device__ __forceinline__ float rcp_nr(float x) {
+    const float y = __builtin_amdgcn_rcpf(x);
+    return fmaf(fmaf(-x, y, 1.0f), y, y);
+}
+
+// 1.0f / sqrtf(x), bit for bit, for any x: the short sequence inside its verified range, the IEEE
+// expansion outside (a branch no lane takes for real rays: x = |d|^2 of a ray direction).
+__device__ __forceinline__ float rsqrt_rn(float x) {
+    if (x >= 0x1p-105f && x < INFINITY) return rcp_nr(sqrt_fix(x));
+    return 1.0f / sqrtf(x);
+}
+
+// 1.0f / sqrtf(r2) for the unit-sphere draw's r2 = |p|^2 < 1: a coordinate 2u - 1 of the draw is
+// 0 or at least 2^-24 in magnitude (u = float(s)*2^-32, float(s) a multiple of 128 near 2^31),
+// so r2 is +0 or >= 2^-48 (a sum of squares, never -0), inside the verified range apart from +0
+// (1/+0 = +inf).
+__device__ __forceinline__ float rsqrt_unit_draw(float r2) {
+    return r2 == 0.0f ? INFINITY : rcp_nr(sqrt_fix(r2));
+}
+
 // Short-cycle escape of the rejection loops (pt_oracle.c PO_ESCAPE).
 __device__ __forceinline__ void escape_cycle(uint32_t &s, unsigned tries) {
     if ((tries & 63u) == 0u) s ^= 0x9E3779B9u;
@@ -252,7 +292,7 @@ __device__ __forceinline__ void store_radiance(float *scratch, unsigned item, fl
 
 // Sky gradient on a miss (RayTracer.h:593-595), times throughput.
 __device__ __forceinline__ void sky(const Ray &r, float tr, float tg, float tb, float &L0, float &L1, float &L2) {
-    const float uy = (1.0f / sqrtf(fdot(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz))) * r.dy;
+    const float uy = rsqrt_rn(fdot(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz)) * r.dy;
     const float al = 0.5f * (uy + 1.0f);
     const float bl = 1.0f - al;
     L0 = tr * fmaf(al, 0.5f, bl);
@@ -321,7 +361,7 @@ __device__ __forceinline__ bool scatter(Ray &r, float t, int prim, const float4 
     const int kind = FULL ? __float_as_int(m0.w) : int(kLambertian);
     if (kind == kMetal) {  // Metal::scatter, :496-501
         const float fuzz = mats[2 * m + 1].x;
-        const float il = 1.0f / sqrtf(fdot(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz));
+        const float il = rsqrt_rn(fdot(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz));
         const float ux = r.dx * il, uy = r.dy * il, uz = r.dz * il;
         const float k = 2.0f * fdot(ux, uy, uz, nx, ny, nz);  // reflect, :174-176
         float qx, qy, qz;
@@ -336,7 +376,7 @@ __device__ __forceinline__ bool scatter(Ray &r, float t, int prim, const float4 
     } else if (kind == kDielectric) {  // Dielectric::scatter, :512-530 (attenuation 1)
         const float ir = mats[2 * m + 1].y;
         const float ratio = front ? (1.0f / ir) : ir;
-        const float il = 1.0f / sqrtf(fdot(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz));
+        const float il = rsqrt_rn(fdot(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz));
         const float ux = r.dx * il, uy = r.dy * il, uz = r.dz * il;
         const float cosT = fminf(fdot(-ux, -uy, -uz, nx, ny, nz), 1.0f);
         const float sinT = sqrtf(1.0f - cosT * cosT);
@@ -362,7 +402,7 @@ __device__ __forceinline__ bool scatter(Ray &r, float t, int prim, const float4 
     } else {  // Lambertian::scatter, :477-484: n + unit(random_in_unit_sphere), 1e-8 fallback
         float qx, qy, qz;
         const float r2 = rius<STATS>(rng, qx, qy, qz, pc, rngTable);
-        const float inv = 1.0f / sqrtf(r2);  // unit_vector = (1/len)*v, :137-139,151-153
+        const float inv = rsqrt_unit_draw(r2);  // unit_vector = (1/len)*v, :137-139,151-153
         sx = nx + qx * inv;
         sy = ny + qy * inv;
         sz = nz + qz * inv;
