@@ -221,6 +221,10 @@ enum {
     , HIPPT_OPT_PIXEL_FORMAT = 25   /* output frame words of the hipptRenderFrames* calls: HIPPT_PIXEL_ARGB
                                        (default, the CUDA backend's) or HIPPT_PIXEL_RGBA8 (the GL / Vulkan
                                        backends'); cudaPathTracerRender always writes ARGB */
+    , HIPPT_OPT_CAMERA_POOL = 26    /* megakernel over a 4-wide float-node tree: each wave generates the camera
+                                       rays of its next 64 samples with all lanes at once into an LDS pool
+                                       instead of one by one as paths end (1), or not (0); -1 (default):
+                                       automatic (on for LDS-resident scenes).  Same results either way */
 };
 /* Output frame word formats (HIPPT_OPT_PIXEL_FORMAT).  Both map an accumulated colour c to
  * sqrt(clamp(c, 0, 1)) per channel.

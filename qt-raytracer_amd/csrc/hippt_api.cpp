@@ -136,6 +136,7 @@ struct State {
     int ldsTopNodes = -1;  // top-of-tree nodes copied into LDS for global-memory trees (-1: automatic)
     bool rngTable = false;  // memoized random_in_unit_sphere (HIPPT_OPT_RNG_TABLE)
     int pixelFormat = HIPPT_PIXEL_ARGB;  // output frame words (HIPPT_OPT_PIXEL_FORMAT)
+    int cameraPool = -1;  // megakernel camera-ray pool (HIPPT_OPT_CAMERA_POOL; -1: automatic)
     std::vector<std::pair<int, uint32_t *>> rngTables;  // per device, built on first use
     unsigned activeTopBytes = 0;  // of the last mesh render (hipptGetOption HIPPT_INFO_*)
     int activeBlocksPerCu = 0;
@@ -650,6 +651,14 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 // breadth-first prefix of the node array that the LDS budget of the resident blocks
                 // leaves beside the stack (automatic), or HIPPT_OPT_LDS_TOP_NODES nodes.  The
                 // wavefront keeps its 8-bit nodes (blob70k: 8.28 G 8-bit, 7.53 G float, r2za).
+                // Camera-ray pool (megakernel, 4-wide float nodes): on by default for LDS-resident
+                // scenes; a tree in global memory gives its spare LDS to the top of the tree instead.
+                // Pinhole cameras at a nonzero origin start every ray at cam.origin exactly
+                // (origin + 0*offset), so their pool entries carry no origin.
+                const bool pool = s.pathMode == 0 && wide && !quant && (s.cameraPool == 1 || (s.cameraPool == -1 && ldsScene));
+                const bool pinhole = cam.lens_radius == 0.0f && cam.origin[0] != 0.0f && cam.origin[1] != 0.0f &&
+                                     cam.origin[2] != 0.0f;
+                const int poolWords = pool ? (pinhole ? hippt::kPoolWordsPinhole : hippt::kPoolWordsFull) : 0;
                 unsigned topBytes = 0;
                 if (topTree && s.ldsTopNodes != 0) {
                     const size_t nodeBytes = quant ? 64 : 128;
@@ -657,7 +666,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                     if (s.ldsTopNodes > 0) {
                         n = std::min(n, size_t(s.ldsTopNodes));
                     } else {
-                        const size_t stackBytes = hippt::mesh_lds_bytes(stackDepth, 0, 0, true);
+                        const size_t stackBytes = hippt::mesh_lds_bytes(stackDepth, 0, 0, true, 0, 0, poolWords);
                         const size_t budget = hippt::mesh_lds_block_budget();
                         n = std::min(n, budget > stackBytes ? (budget - stackBytes) / nodeBytes : 0);
                     }
@@ -665,13 +674,13 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 }
                 const long long occKey =
                     occupancy_key(s.scene.version, stackDepth, ldsScene, s.scene.full, wide, quant, spills) ^
-                    ((long long)topBytes << 40);
+                    ((long long)topBytes << 40) ^ ((long long)poolWords << 36);
                 if (c.occKey != occKey) {
                     const int ln = ldsScene ? numNodes : 0, lt = ldsScene ? numTris : 0, lm = ldsScene ? numMats : 0;
                     c.meshBlocksPerCu[0] = hippt::mesh_blocks_per_cu(false, s.scene.full, wide, quant, stackDepth,
-                                                                     ln, lt, spills, topBytes, lm);
+                                                                     ln, lt, spills, topBytes, lm, poolWords);
                     c.meshBlocksPerCu[1] = hippt::mesh_blocks_per_cu(true, s.scene.full, wide, quant, stackDepth,
-                                                                     ln, lt, spills, topBytes, lm);
+                                                                     ln, lt, spills, topBytes, lm, poolWords);
                     c.occKey = occKey;
                 }
                 s.activeTopBytes = topBytes;
@@ -730,6 +739,10 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.stackCap = stackCap;
                         p.topBytes = topBytes;
                         p.rngTable = nullptr;
+                        p.poolWords = poolWords;
+                        p.poolOffset = unsigned(hippt::mesh_lds_bytes(stackDepth, ldsScene ? numNodes : 0,
+                                                                      ldsScene ? numTris : 0, wide, topBytes,
+                                                                      ldsScene ? numMats : 0));
                         if (s.rngTable && !rng_table(c, &p.rngTable, err)) return false;
                         if (s.pathMode == 1) {
                             if (!run_wavefront(c, p, cnt, spills, s.scene.stackBound4 + 3, err)) return false;
@@ -1316,6 +1329,10 @@ extern "C" bool hipptSetOption(int key, long long value) {
         if (value != HIPPT_PIXEL_ARGB && value != HIPPT_PIXEL_RGBA8) return false;
         s.pixelFormat = int(value);
         return true;
+    case HIPPT_OPT_CAMERA_POOL:
+        if (value < -1 || value > 1) return false;
+        s.cameraPool = int(value);
+        return true;
     default: return false;
     }
 }
@@ -1353,6 +1370,7 @@ extern "C" long long hipptGetOption(int key) {
     case HIPPT_OPT_BVH_LEAF4: return s.bvh.maxLeaf4;
     case HIPPT_OPT_RNG_TABLE: return s.rngTable ? 1 : 0;
     case HIPPT_OPT_PIXEL_FORMAT: return s.pixelFormat;
+    case HIPPT_OPT_CAMERA_POOL: return s.cameraPool;
     case HIPPT_INFO_LDS_TOP_BYTES: return s.activeTopBytes;
     case HIPPT_INFO_BLOCKS_PER_CU: return s.activeBlocksPerCu;
     default: return -1;

@@ -69,6 +69,11 @@ struct MeshParams {
     // random_in_unit_sphere memoized (null: the rejection loop): entry 2^32-word table, see
     // launch_rng_table
     const uint32_t *rngTable;
+    // camera-ray pool (HIPPT_OPT_CAMERA_POOL): each wave's 64 pre-generated camera rays at LDS byte
+    // poolOffset + wave * poolWords * 256, poolWords fields of 64 words each: item, rng, d.xyz and,
+    // unless the camera is a pinhole at a nonzero origin (every ray starts at cam.origin), o.xyz
+    unsigned poolOffset;
+    int poolWords;
 };
 
 // Running average + tonemap over a batch of per-sample radiances
@@ -105,8 +110,12 @@ constexpr size_t kRngTableBytes = size_t(4) << 32;
 hipError_t launch_rng_table(uint32_t *table, hipStream_t s);
 // Resident mesh-kernel blocks per CU for a given LDS stack depth and LDS scene size.
 int mesh_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,
-                       int ldsTris, bool spill, unsigned topBytes = 0, int ldsMats = 0);
-size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide, unsigned topBytes = 0, int ldsMats = 0);
+                       int ldsTris, bool spill, unsigned topBytes = 0, int ldsMats = 0, int poolWords = 0);
+size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide, unsigned topBytes = 0, int ldsMats = 0,
+                      int poolWords = 0);
+// camera-ray pool words per ray: item, rng, direction (+ origin unless every ray starts at the
+// camera origin)
+constexpr int kPoolWordsPinhole = 5, kPoolWordsFull = 8;
 // LDS bytes per block that keep the persistent grid's resident blocks within a CU's LDS
 size_t mesh_lds_block_budget();
 size_t mesh_lds_scene_limit();

@@ -196,7 +196,35 @@ __device__ unsigned long long g_timeline[65536 * 6];
 #ifndef HIPPT_WIDE_WAVES_PER_EU
 #define HIPPT_WIDE_WAVES_PER_EU 7
 #endif
-template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE, bool QUANT, bool SPILL = true>
+// Camera-ray pool (POOL, HIPPT_OPT_CAMERA_POOL): a refill happens when a lane's path ends, so only
+// the lanes whose paths ended together generate camera rays, at ~30% SIMD efficiency (Cornell,
+// tools/phase_profile.py).  With the pool, the wave generates the camera rays of its next 64 work
+// items with all lanes at once into LDS (one entry per lane, fields 64 words apart: conflict-free),
+// and refilling lanes take the next entries in order; the pool is regenerated when a refill needs
+// more entries than it holds (those lanes take the rest of the old pool first, then the new one).
+// Items are claimed from the work queue in the same order as without the pool and every claimed
+// item is traced, so the results are the same.
+template <bool POOL>
+__device__ __forceinline__ void pool_take(const MeshParams &P, const float *pool, unsigned k, unsigned &item, Ray &r,
+                                          uint32_t &rng) {
+    item = __float_as_uint(pool[k]);
+    if (item == kNone) return;
+    rng = __float_as_uint(pool[64 + k]);
+    r.dx = pool[128 + k];
+    r.dy = pool[192 + k];
+    r.dz = pool[256 + k];
+    if (P.poolWords == kPoolWordsFull) {
+        r.ox = pool[320 + k];
+        r.oy = pool[384 + k];
+        r.oz = pool[448 + k];
+    } else {
+        r.ox = P.cam.origin[0];
+        r.oy = P.cam.origin[1];
+        r.oz = P.cam.origin[2];
+    }
+}
+
+template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE, bool QUANT, bool SPILL = true, bool POOL = false>
 __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_EU : HIPPT_MESH_WAVES_PER_EU) HIPPT_SGPR_ATTR void mesh_kernel(MeshParams P) {
     static_assert(!QUANT || (WIDE && !LDS_SCENE), "quantized nodes: 4-wide global-memory traversal only");
 #ifdef HIPPT_DEBUG_TIMELINE
@@ -251,6 +279,11 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     constexpr int nodeF4 = LDS_SCENE ? ldsNodeF4 : (WIDE ? (QUANT ? 4 : 8) : 4);
     const SpillArea S{P.spill, (blockIdx.x * unsigned(kMeshBlock) + threadIdx.x) * unsigned(P.spillCap), P.stackCap};
 
+    // this wave's camera-ray pool (POOL): entries [poolNext, 64) not taken yet (wave-uniform)
+    float *const pool = reinterpret_cast<float *>(reinterpret_cast<char *>(lds) + P.poolOffset) +
+                        (threadIdx.x >> 6) * unsigned(P.poolWords * 64);
+    unsigned poolNext = 64;
+
     WorkQueue Q;
     queue_begin(Q, P.totalItems, P.chunk);
     unsigned item = kNone;
@@ -275,7 +308,57 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     for (;;) {
         prof<STATS>(pc, 0);
         // ---- refill: every lane whose sample ended takes the next (pixel, frame) -------------
-        if (__ballot(need)) {
+        if (POOL) {
+            const unsigned long long m = __ballot(need);
+            if (m) {
+                const unsigned n = unsigned(__popcll(m));
+                const unsigned rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
+                const unsigned avail = 64u - poolNext;
+                const bool took = need;
+                if (need && rank < avail) {
+                    need = false;
+                    pool_take<POOL>(P, pool, poolNext + rank, item, r, rng);
+                }
+                if (n > avail) {
+                    // the camera rays of the wave's next 64 items, every lane at once
+                    const unsigned it = queue_fetch(true, Q, P.queue, P.totalItems, P.chunk);
+#ifdef HIPPT_DEBUG_TIMELINE
+                    if (!tlDrained && __ballot(it == kNone)) tlDrained = __builtin_amdgcn_s_memrealtime();
+                    tlItems += __popcll(__ballot(it != kNone));
+#endif
+                    Ray c{};
+                    uint32_t crng = 0;
+                    if (it != kNone) {
+                        prof<STATS>(pc, 1);
+                        camera_sample(P, it, c, crng);
+                    }
+                    const unsigned k = __lane_id();
+                    pool[k] = __uint_as_float(it);
+                    pool[64 + k] = __uint_as_float(crng);
+                    pool[128 + k] = c.dx;
+                    pool[192 + k] = c.dy;
+                    pool[256 + k] = c.dz;
+                    if (P.poolWords == kPoolWordsFull) {
+                        pool[320 + k] = c.ox;
+                        pool[384 + k] = c.oy;
+                        pool[448 + k] = c.oz;
+                    }
+                    poolNext = n - avail;
+                    if (need) {
+                        need = false;
+                        pool_take<POOL>(P, pool, rank - avail, item, r, rng);
+                    }
+                } else {
+                    poolNext += n;
+                }
+                if (took && item != kNone) {
+                    tr = tg = tb = 1.0f;
+                    depth = 0;
+                    prepare(r);
+                    begin(T);
+                }
+            }
+        } else if (__ballot(need)) {
             const unsigned it = queue_fetch(need, Q, P.queue, P.totalItems, P.chunk);
 #ifdef HIPPT_DEBUG_TIMELINE
             if (!tlDrained && __ballot(need && it == kNone)) tlDrained = __builtin_amdgcn_s_memrealtime();
@@ -429,10 +512,11 @@ hipError_t launch_sphere4(const Sphere4Params &p, hipStream_t s) {
 
 // Stack: one spare slot per lane above the deepest level for the speculative far-child
 // write; then (LDS_SCENE) the scene copy.
-size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide, unsigned topBytes, int ldsMats) {
+size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide, unsigned topBytes, int ldsMats,
+                      int poolWords) {
     return size_t(stackDepth + 1) * kMeshBlock * sizeof(int) +
            size_t(ldsNodes) * (wide ? kLdsNode4F4 : kLdsNodeF4) * 16 + size_t(ldsTris) * (3 + 1) * 16 + topBytes +
-           size_t(ldsMats) * 2 * 16;
+           size_t(ldsMats) * 2 * 16 + size_t(poolWords) * kMeshBlock * sizeof(float);
 }
 
 size_t mesh_lds_scene_limit() { return 24u << 10; }
@@ -448,21 +532,26 @@ using MeshFn = void (*)(MeshParams);
 // node formats: 2-wide, 4-wide float, 4-wide quantized (global memory only)
 // 4-wide trees whose stack bound fits the LDS capacity run a variant without the spill/refill
 // code (timed builds; the counting builds keep one variant, the results are the same)
-template <bool STATS, bool FULL, bool SPILL>
+// (the camera-ray pool: 4-wide float-node kernels)
+template <bool STATS, bool FULL, bool SPILL, bool POOL>
 static MeshFn mesh_fn_wide(bool lds, bool quant) {
-    if (lds) return mesh_kernel<STATS, true, FULL, true, false, SPILL>;
-    return quant ? mesh_kernel<STATS, false, FULL, true, true, SPILL> : mesh_kernel<STATS, false, FULL, true, false, SPILL>;
+    if (lds) return mesh_kernel<STATS, true, FULL, true, false, SPILL, POOL>;
+    return quant ? mesh_kernel<STATS, false, FULL, true, true, SPILL>
+                 : mesh_kernel<STATS, false, FULL, true, false, SPILL, POOL>;
 }
 template <bool STATS, bool FULL>
-static MeshFn mesh_fn_fmt(bool lds, bool wide, bool quant, bool spill) {
+static MeshFn mesh_fn_fmt(bool lds, bool wide, bool quant, bool spill, bool pool) {
     if (!wide) return lds ? mesh_kernel<STATS, true, FULL, false, false> : mesh_kernel<STATS, false, FULL, false, false>;
-    if (STATS || spill) return mesh_fn_wide<STATS, FULL, true>(lds, quant);
-    return mesh_fn_wide<STATS, FULL, false>(lds, quant);
+    if (STATS || spill)
+        return pool ? mesh_fn_wide<STATS, FULL, true, true>(lds, quant) : mesh_fn_wide<STATS, FULL, true, false>(lds, quant);
+    return pool ? mesh_fn_wide<STATS, FULL, false, true>(lds, quant) : mesh_fn_wide<STATS, FULL, false, false>(lds, quant);
 }
-static MeshFn mesh_fn(bool count, bool lds, bool full, bool wide, bool quant, bool spill) {
+static MeshFn mesh_fn(bool count, bool lds, bool full, bool wide, bool quant, bool spill, bool pool) {
     if (count)
-        return full ? mesh_fn_fmt<true, true>(lds, wide, quant, spill) : mesh_fn_fmt<true, false>(lds, wide, quant, spill);
-    return full ? mesh_fn_fmt<false, true>(lds, wide, quant, spill) : mesh_fn_fmt<false, false>(lds, wide, quant, spill);
+        return full ? mesh_fn_fmt<true, true>(lds, wide, quant, spill, pool)
+                    : mesh_fn_fmt<true, false>(lds, wide, quant, spill, pool);
+    return full ? mesh_fn_fmt<false, true>(lds, wide, quant, spill, pool)
+                : mesh_fn_fmt<false, false>(lds, wide, quant, spill, pool);
 }
 
 hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hipStream_t s) {
@@ -471,16 +560,17 @@ hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hip
     const bool lds = p.ldsScene != 0;
     if (p.topBytes && (lds || !p.wide || p.topBytes % (p.wide == 2 ? 64u : 128u) || p.topBytes > (unsigned(p.numNodes) << (p.wide == 2 ? 6 : 7))))
         return hipErrorInvalidValue;
-    const size_t bytes =
-        mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0, p.wide != 0, p.topBytes, lds ? p.numMats : 0);
-    const MeshFn fn = mesh_fn(countTraversal, lds, p.full != 0, p.wide != 0, p.wide == 2 && !lds, p.spill != nullptr);
-    if (p.wide && (lds || p.topBytes)) {
+    const bool pool = p.poolWords != 0;
+    if (pool && (p.wide != 1 || (p.poolWords != kPoolWordsPinhole && p.poolWords != kPoolWordsFull))) return hipErrorInvalidValue;
+    const size_t bytes = mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0, p.wide != 0, p.topBytes,
+                                        lds ? p.numMats : 0, p.poolWords);
+    if (pool && p.poolOffset != bytes - size_t(p.poolWords) * kMeshBlock * sizeof(float)) return hipErrorInvalidValue;
+    const MeshFn fn = mesh_fn(countTraversal, lds, p.full != 0, p.wide != 0, p.wide == 2 && !lds, p.spill != nullptr, pool);
+    if (p.wide && (lds || p.topBytes || pool)) {
         const hipError_t e = check_lds_at_zero(reinterpret_cast<const void *>(fn));
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(mesh_fn(countTraversal, lds, p.full != 0, p.wide != 0, p.wide == 2 && !lds, p.spill != nullptr),
-                       dim3(blocks),
-                       dim3(kMeshBlock), bytes, s, p);
+    hipLaunchKernelGGL(fn, dim3(blocks), dim3(kMeshBlock), bytes, s, p);
     return hipGetLastError();
 }
 
@@ -493,12 +583,12 @@ hipError_t launch_combine(const CombineParams &p, hipStream_t s) {
 }
 
 int mesh_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,
-                       int ldsTris, bool spill, unsigned topBytes, int ldsMats) {
+                       int ldsTris, bool spill, unsigned topBytes, int ldsMats, int poolWords) {
     int n = 0;
     const bool lds = ldsNodes > 0;
-    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, wide, topBytes, ldsMats);
+    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, wide, topBytes, ldsMats, poolWords);
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &n, mesh_fn(countTraversal, lds, full, wide, quant && wide && !lds, spill), kMeshBlock, bytes);
+        &n, mesh_fn(countTraversal, lds, full, wide, quant && wide && !lds, spill, poolWords != 0), kMeshBlock, bytes);
     if (e != hipSuccess || n <= 0) n = 1;
     // the query ignores the trap handler's SGPRs (kMaxResidentBlocks): a larger persistent grid
     // leaves blocks waiting for a slot until others finish

@@ -29,7 +29,8 @@ def pt():
                  (hippt.OPT_NODE_EXIT, -1), (hippt.OPT_BVH_SAH, 1), (hippt.OPT_BVH_WIDTH, 0),
                  (hippt.OPT_STACK_CAP, 0), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_LDS_TOP_NODES, -1),
                  (hippt.OPT_RNG_TABLE, 0), (hippt.OPT_BVH_COLLAPSE, 0), (hippt.OPT_BVH_NODE_COST, 200),
-                 (hippt.OPT_BVH_LEAF4, 4), (hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_ARGB)):
+                 (hippt.OPT_BVH_LEAF4, 4), (hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_ARGB),
+                 (hippt.OPT_CAMERA_POOL, -1)):
         t.setOption(k, v)
     t.resetStats()
     yield t
@@ -370,6 +371,38 @@ def test_rng_table_and_sah_collapse_do_not_change_results(pt, name):
                 assert pt.renderFrames(3, 8)
                 got = pt.readback()
                 _assert_same(got[0], got[1], ora[0], ora[1])
+
+
+@pytest.mark.parametrize("name,variant", [
+    ("cornell34", "pinhole"),       # pool entries without the origin (every ray starts at cam.origin)
+    ("cornell34", "zero_origin"),   # a pinhole at an origin with a zero component: origin stored
+    ("cornell34", "lens"),          # aperture > 0: origin stored
+    ("cornell_mixed", "pinhole"),   # general kernel, LDS scene
+    ("random_scene", "lens"),       # general kernel, tree in global memory
+    ("blob70k", "pinhole"),         # Lambertian kernel, tree in global memory (+ LDS top)
+])
+def test_camera_pool_does_not_change_results(pt, name, variant):
+    """The megakernel's camera-ray pool (HIPPT_OPT_CAMERA_POOL: each wave generates the camera rays
+    of its next 64 samples at once into LDS) gives the oracle's image bit for bit, on and off, at
+    sizes whose item count is not a multiple of 64 (a partly filled last pool)."""
+    sc = scenes.get_scene(name)
+    if variant == "zero_origin":
+        sc.lookfrom = (0.0, 278.0, -800.0)
+    elif variant == "lens" and name == "cornell34":
+        sc.aperture = 25.0
+        sc.focus = 800.0
+    w, h = (37, 23) if name != "cornell34" else (53, 29)
+    ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
+    pt.uploadMesh(sc)
+    for pool in (1, 0, -1):
+        pt.setOption(hippt.OPT_CAMERA_POOL, pool)
+        assert pt.initialize(w, h), pt.lastError()
+        assert pt.renderFrames(3, 8), pt.lastError()
+        got = pt.readback()
+        _assert_same(got[0], got[1], ora[0], ora[1])
+        st = pt.stats()
+        assert st["segments"] == ora[2] and st["pixelSamples"] == ora[3]
+        pt.resetStats()
 
 
 @pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene"])

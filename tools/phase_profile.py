@@ -21,7 +21,7 @@ KEYS = {"wave": hippt.OPT_WAVE_THRESHOLD, "chunk": hippt.OPT_CHUNK, "lds": hippt
         "width": hippt.OPT_BVH_WIDTH, "stackcap": hippt.OPT_STACK_CAP, "leafexit": hippt.OPT_LEAF_EXIT,
         "nodeexit": hippt.OPT_NODE_EXIT, "quant": hippt.OPT_BVH_QUANT,
         "top": hippt.OPT_LDS_TOP_NODES, "collapse": hippt.OPT_BVH_COLLAPSE,
-        "ncost": hippt.OPT_BVH_NODE_COST}
+        "ncost": hippt.OPT_BVH_NODE_COST, "pool": hippt.OPT_CAMERA_POOL}
 
 
 def main():
