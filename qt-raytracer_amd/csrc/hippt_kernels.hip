@@ -298,7 +298,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     T.bestI = -1;
     T.bestO = 0x7fffffff;
     float tr = 1, tg = 1, tb = 1;
-    bool need = true;
+    bool need = true, fresh = false;
     // per-lane counts fit 32 bits (a lane traces a few thousand segments per launch); widened
     // for the wave sum
     unsigned segs = 0, samples = 0;
@@ -354,8 +354,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                 if (took && item != kNone) {
                     tr = tg = tb = 1.0f;
                     depth = 0;
-                    prepare(r);
-                    begin(T);
+                    fresh = true;
                 }
             }
         } else if (__ballot(need)) {
@@ -372,10 +371,16 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                     camera_sample(P, it, r, rng);
                     tr = tg = tb = 1.0f;
                     depth = 0;
-                    prepare(r);
-                    begin(T);
+                    fresh = true;
                 }
             }
+        }
+        // new rays (refilled or scattered): one place, so a pass with lanes of both kinds runs
+        // the reciprocals once
+        if (fresh) {
+            fresh = false;
+            prepare(r);
+            begin(T);
         }
         if (!__any(busy(T))) break;
 
@@ -395,15 +400,30 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
             ++segs;
             bool finished = false;
             float Lr = 0.0f, Lg = 0.0f, Lb = 0.0f;
-            if (T.bestI < 0) {
+            if (!FULL) {
+                // Lambertian triangles: the sky's 1/sqrt(|d|^2) and the scatter's 1/sqrt(|q|^2) as one
+                // sequence for both kinds of lanes (the draw first: no other draw precedes it)
+                const bool miss = T.bestI < 0;
+                // depth exhausted: contributes 0 (RayTracer.h:582-583)
+                const bool scat = !miss && ++depth < P.maxDepth;
+                float qx = 0.0f, qy = 0.0f, qz = 0.0f;
+                float x = fdot(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz);
+                if (scat) x = rius<STATS>(rng, qx, qy, qz, pc, P.rngTable);
+                const float inv = rsqrt_rn(x);
+                if (miss) sky_inv(r, inv, tr, tg, tb, Lr, Lg, Lb);
+                if (scat) {
+                    lambert_apply(r, T.bestT, T.bestI, shade, mats, qx, qy, qz, inv, tr, tg, tb);
+                    fresh = true;
+                }
+                finished = !scat;
+            } else if (T.bestI < 0) {
                 sky(r, tr, tg, tb, Lr, Lg, Lb);
                 finished = true;
             } else if (++depth >= P.maxDepth) {
                 finished = true;  // depth exhausted: contributes 0 (RayTracer.h:582-583)
             } else if (scatter<FULL, STATS>(r, T.bestT, T.bestI, shade, tris, mats, rng, tr, tg, tb, pc,
                                             P.rngTable)) {
-                prepare(r);
-                begin(T);
+                fresh = true;
             } else {
                 finished = true;  // absorbed: contributes 0 (RayTracer.h:590)
             }

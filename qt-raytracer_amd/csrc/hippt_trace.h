@@ -290,7 +290,17 @@ __device__ __forceinline__ void store_radiance(float *scratch, unsigned item, fl
     *reinterpret_cast<float3 *>(scratch + 3 * size_t(item)) = make_float3(r, g, b);
 }
 
-// Sky gradient on a miss (RayTracer.h:593-595), times throughput.
+// Sky gradient on a miss (RayTracer.h:593-595), times throughput; `inv` = 1/sqrtf(|d|^2).
+__device__ __forceinline__ void sky_inv(const Ray &r, float inv, float tr, float tg, float tb, float &L0, float &L1,
+                                        float &L2) {
+    const float uy = inv * r.dy;
+    const float al = 0.5f * (uy + 1.0f);
+    const float bl = 1.0f - al;
+    L0 = tr * fmaf(al, 0.5f, bl);
+    L1 = tg * fmaf(al, 0.7f, bl);
+    L2 = tb * fmaf(al, 1.0f, bl);
+}
+
 __device__ __forceinline__ void sky(const Ray &r, float tr, float tg, float tb, float &L0, float &L1, float &L2) {
     const float uy = rsqrt_rn(fdot(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz)) * r.dy;
     const float al = 0.5f * (uy + 1.0f);
@@ -422,6 +432,39 @@ __device__ __forceinline__ bool scatter(Ray &r, float t, int prim, const float4 
     r.dy = sy;
     r.dz = sz;
     return true;
+}
+
+// Lambertian scatter at a triangle hit (the FULL=false part of scatter() after its unit-sphere
+// draw q, |q|^2 = r2, inv = 1/sqrtf(r2)): the megakernel computes the draw first and shares one
+// 1/sqrt sequence between the lanes that scatter and those that take the sky.
+__device__ __forceinline__ void lambert_apply(Ray &r, float t, int prim, const float4 *shade, const float4 *mats,
+                                              float qx, float qy, float qz, float inv, float &tr, float &tg,
+                                              float &tb) {
+    const float4 sh = shade[prim];
+    const int m = __float_as_int(sh.w);
+    const float px = fmaf(t, r.dx, r.ox), py = fmaf(t, r.dy, r.oy), pz = fmaf(t, r.dz, r.oz);  // Ray::at
+    float nx = sh.x, ny = sh.y, nz = sh.z;
+    if (!(fdot(r.dx, r.dy, r.dz, nx, ny, nz) < 0.0f)) {  // set_face_normal, :215-218
+        nx = -nx;
+        ny = -ny;
+        nz = -nz;
+    }
+    const float4 m0 = mats[2 * m];
+    float sx = nx + qx * inv, sy = ny + qy * inv, sz = nz + qz * inv;  // :477-484
+    if (fdot(sx, sy, sz, sx, sy, sz) < 1e-8f) {
+        sx = nx;
+        sy = ny;
+        sz = nz;
+    }
+    tr *= m0.x;
+    tg *= m0.y;
+    tb *= m0.z;
+    r.ox = px;
+    r.oy = py;
+    r.oz = pz;
+    r.dx = sx;
+    r.dy = sy;
+    r.dz = sz;
 }
 
 // Sphere::hit (RayTracer.h:289-314) root selection in the contract's FP32 form
