@@ -225,6 +225,10 @@ enum {
                                        rays of its next 64 samples with all lanes at once into an LDS pool
                                        instead of one by one as paths end (1), or not (0); -1 (default):
                                        automatic (on for LDS-resident scenes).  Same results either way */
+    , HIPPT_OPT_FUSE_COMBINE = 27   /* megakernel: a batch's running average + tonemap runs inside the next
+                                       batch's launch on the same device (beside its paths) instead of as a
+                                       launch of its own, whenever nothing reads the image in between (1), or
+                                       never (0); -1 (default): automatic.  Same results either way */
 };
 /* Output frame word formats (HIPPT_OPT_PIXEL_FORMAT).  Both map an accumulated colour c to
  * sqrt(clamp(c, 0, 1)) per channel.

@@ -46,7 +46,10 @@ constexpr int kSpillStackCap = 13;
 // of the node array is the top of the tree; trees read from global memory keep such a prefix in
 // LDS (HIPPT_OPT_LDS_TOP_NODES)
 constexpr int kTopOrderNodes = 1365;  // 6 complete levels
-constexpr size_t kQueueBytes = 8 * 32 * sizeof(unsigned);  // hippt_trace.h kQueues x kQueueStride
+// hippt_trace.h kQueues x kQueueStride work counters, then (its own line) the fused combine's
+// chunk counter (MeshParams::combCtr)
+constexpr size_t kCombCtrWord = 8 * 32;
+constexpr size_t kQueueBytes = (kCombCtrWord + 32) * sizeof(unsigned);
 
 struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
@@ -60,6 +63,14 @@ struct Ctx {
     uint32_t *out = nullptr;
     float *scratch = nullptr;
     size_t scratchBytes = 0;
+    // Megakernel batches defer their combine (running average + tonemap) into the next batch's
+    // launch on this context, which does it between its paths (MeshParams::comb); the two batches'
+    // per-sample radiances then live in two buffers.  Flushed (a combine launch of its own) before
+    // anything reads or resets the image: sync, present, copies, reset, a non-megakernel batch.
+    float *scratchAlt = nullptr;
+    size_t scratchAltBytes = 0;
+    hippt::CombineParams deferred{};
+    bool hasDeferred = false;
     unsigned *queue = nullptr;
     unsigned long long *stats = nullptr;
     int sceneVersion = -1;
@@ -137,6 +148,7 @@ struct State {
     bool rngTable = false;  // memoized random_in_unit_sphere (HIPPT_OPT_RNG_TABLE)
     int pixelFormat = HIPPT_PIXEL_ARGB;  // output frame words (HIPPT_OPT_PIXEL_FORMAT)
     int cameraPool = -1;  // megakernel camera-ray pool (HIPPT_OPT_CAMERA_POOL; -1: automatic)
+    int fuseCombine = -1;  // combine inside the next megakernel launch (HIPPT_OPT_FUSE_COMBINE)
     std::vector<std::pair<int, uint32_t *>> rngTables;  // per device, built on first use
     unsigned activeTopBytes = 0;  // of the last mesh render (hipptGetOption HIPPT_INFO_*)
     int activeBlocksPerCu = 0;
@@ -242,6 +254,10 @@ void destroy_ctx(Ctx &c) {
     (void)hipFree(c.accum);
     (void)hipFree(c.out);
     (void)hipFree(c.scratch);
+    (void)hipFree(c.scratchAlt);
+    c.scratchAlt = nullptr;
+    c.scratchAltBytes = 0;
+    c.hasDeferred = false;
     (void)hipFree(c.queue);
     (void)hipFree(c.stats);
     (void)hipFree(c.wfPool);
@@ -575,6 +591,37 @@ bool copy_rows_async(Ctx &c, void *dstFrame, const void *src, size_t bytes, cons
     return true;
 }
 
+// The deferred combine of a context as a launch of its own (see Ctx::deferred).
+bool flush_deferred(Ctx &c, const char **err) {
+    if (!c.hasDeferred) return true;
+    c.hasDeferred = false;
+    HIP_TRY(hipSetDevice(c.device));
+    EventPair ev;
+    if (!next_events(c, ev, err)) return false;
+    HIP_TRY(hipEventRecord(ev.a, c.stream));
+    HIP_TRY(hippt::launch_combine(c.deferred, c.stream));
+    HIP_TRY(hipEventRecord(ev.b, c.stream));
+    c.pending.push_back({1, ev});
+    return true;
+}
+
+// A per-sample radiance buffer of at least `need` bytes that the deferred combine does not read.
+bool batch_scratch(Ctx &c, size_t need, float **out, const char **err) {
+    const bool alt = c.hasDeferred && c.deferred.scratch == c.scratch;
+    float *&buf = alt ? c.scratchAlt : c.scratch;
+    size_t &bytes = alt ? c.scratchAltBytes : c.scratchBytes;
+    if (bytes < need) {
+        HIP_TRY(hipStreamSynchronize(c.stream));
+        (void)hipFree(buf);
+        buf = nullptr;
+        bytes = 0;
+        HIP_TRY(hipMalloc(&buf, need));
+        bytes = need;
+    }
+    *out = buf;
+    return true;
+}
+
 bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const char **err) {
     State &s = S();
     if (!s.ready) return fail(err, "HIP path tracer not initialized");
@@ -604,14 +651,6 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 fpb = int(std::min<long long>(fpb, (1LL << 31) / std::max<unsigned>(1, bandPixels)));
                 fpb = std::max(fpb, 1);
                 const size_t need = perFrame * size_t(fpb);
-                if (c.scratchBytes < need) {
-                    HIP_TRY(hipStreamSynchronize(c.stream));
-                    (void)hipFree(c.scratch);
-                    c.scratch = nullptr;
-                    c.scratchBytes = 0;
-                    HIP_TRY(hipMalloc(&c.scratch, need));
-                    c.scratchBytes = need;
-                }
                 const bool cnt = s.countTraversal;
                 // Traversal over the 4-wide tree (HIPPT_OPT_BVH_WIDTH), megakernel and wavefront.
                 // Automatic: 4-wide.  With near/far rows read by the ray's octant, 4-wide beats
@@ -689,16 +728,21 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 for (int b = 0; b < count; b += fpb) {
                     const int nf = std::min(fpb, count - b);
                     const unsigned total = bandPixels * unsigned(nf);
+                    // the megakernel takes the previous batch's combine along; other batches flush it
+                    const bool fuse = maxDepth > 0 && s.pathMode == 0 && s.fuseCombine != 0;
+                    if (!fuse && !flush_deferred(c, err)) return false;
+                    float *scratch = nullptr;
+                    if (!batch_scratch(c, need, &scratch, err)) return false;
                     if (maxDepth <= 0) {
                         // ray_color with depth <= 0 returns black without tracing (RayTracer.h:582-583)
-                        HIP_TRY(hipMemsetAsync(c.scratch, 0, size_t(total) * 3 * sizeof(float), c.stream));
+                        HIP_TRY(hipMemsetAsync(scratch, 0, size_t(total) * 3 * sizeof(float), c.stream));
                     } else {
                         hippt::MeshParams p{};
                         p.nodes = quant ? c.nodes4q : wide ? c.nodes4 : c.nodes;
                         p.tris = c.tris;
                         p.shade = c.shade;
                         p.mats = c.mats;
-                        p.scratch = c.scratch;
+                        p.scratch = scratch;
                         p.queue = c.queue;
                         p.stats = c.stats;
                         p.cam = cam;
@@ -752,6 +796,11 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                             blocks = std::max<long long>(blocks, 1);
                             if (!ensure_spill(c, p, blocks, spills, s.scene.stackBound4 + 3, err)) return false;
                             HIP_TRY(hipMemsetAsync(c.queue, 0, kQueueBytes, c.stream));
+                            if (c.hasDeferred) {
+                                p.comb = c.deferred;
+                                c.hasDeferred = false;
+                            }
+                            p.combCtr = c.queue + kCombCtrWord;
                             EventPair ev;
                             if (!next_events(c, ev, err)) return false;
                             HIP_TRY(hipEventRecord(ev.a, c.stream));
@@ -760,16 +809,14 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                             c.pending.push_back({0, ev});
                         }
                     }
-                    hippt::CombineParams q{c.accum, c.out, c.scratch, bandPixels, total, firstFrame + b, nf, s.pixelFormat};
-                    EventPair ev2;
-                    if (!next_events(c, ev2, err)) return false;
-                    HIP_TRY(hipEventRecord(ev2.a, c.stream));
-                    HIP_TRY(hippt::launch_combine(q, c.stream));
-                    HIP_TRY(hipEventRecord(ev2.b, c.stream));
-                    c.pending.push_back({1, ev2});
+                    c.deferred = hippt::CombineParams{c.accum, c.out, scratch, bandPixels, total, firstFrame + b, nf,
+                                                      s.pixelFormat};
+                    c.hasDeferred = true;
+                    if (!fuse && !flush_deferred(c, err)) return false;
                 }
             }
         }
+        if (copy && !flush_deferred(c, err)) return false;
         if (copy && rows > 0) {
             if (!copy_rows_async(c, s.host, c.out, sizeof(uint32_t), err)) return false;
         }
@@ -780,6 +827,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
 bool sync_locked(const char **err) {
     State &s = S();
     for (Ctx &c : s.ctxs) {
+        if (!flush_deferred(c, err)) return false;
         HIP_TRY(hipSetDevice(c.device));
         HIP_TRY(hipStreamSynchronize(c.stream));
         for (auto &pe : c.pending)
@@ -1110,6 +1158,7 @@ extern "C" bool hipptRenderFramesPresent(int firstFrame, int count, int maxDepth
         HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.present[b]), s.hostCount * sizeof(unsigned),
                               hipHostMallocPortable));
     for (Ctx &c : s.ctxs) {
+        if (!flush_deferred(c, err)) return false;
         HIP_TRY(hipSetDevice(c.device));
         if (!c.presentEv[b]) HIP_TRY(hipEventCreateWithFlags(&c.presentEv[b], hipEventDisableTiming));
         if (!copy_rows_async(c, s.present[b], c.out, sizeof(uint32_t), err)) return false;
@@ -1169,6 +1218,7 @@ extern "C" bool hipptResetAccumulation(const char **err) {
     State &s = S();
     if (!s.ready) return fail(err, "HIP path tracer not initialized");
     for (Ctx &c : s.ctxs) {
+        if (!flush_deferred(c, err)) return false;
         HIP_TRY(hipSetDevice(c.device));
         const size_t px = size_t(c.rows) * size_t(s.width);
         HIP_TRY(hipMemsetAsync(c.accum, 0, px * sizeof(float4), c.stream));
@@ -1333,6 +1383,10 @@ extern "C" bool hipptSetOption(int key, long long value) {
         if (value < -1 || value > 1) return false;
         s.cameraPool = int(value);
         return true;
+    case HIPPT_OPT_FUSE_COMBINE:
+        if (value < -1 || value > 1) return false;
+        s.fuseCombine = int(value);
+        return true;
     default: return false;
     }
 }
@@ -1371,6 +1425,7 @@ extern "C" long long hipptGetOption(int key) {
     case HIPPT_OPT_RNG_TABLE: return s.rngTable ? 1 : 0;
     case HIPPT_OPT_PIXEL_FORMAT: return s.pixelFormat;
     case HIPPT_OPT_CAMERA_POOL: return s.cameraPool;
+    case HIPPT_OPT_FUSE_COMBINE: return s.fuseCombine;
     case HIPPT_INFO_LDS_TOP_BYTES: return s.activeTopBytes;
     case HIPPT_INFO_BLOCKS_PER_CU: return s.activeBlocksPerCu;
     default: return -1;

@@ -27,6 +27,17 @@ struct Sphere4Params {
 // Pixel word formats of the output frame (HIPPT_OPT_PIXEL_FORMAT)
 enum { kPixelArgb = 0, kPixelRgba8 = 1 };
 
+// Running average + tonemap over a batch of per-sample radiances
+// (CudaPathTracerKernel.cu:157-178).
+struct CombineParams {
+    float4 *accum;
+    uint32_t *out;
+    const float *scratch;
+    unsigned bandPixels, totalItems;
+    int firstFrame, frames;
+    int format;  // kPixelArgb / kPixelRgba8
+};
+
 // Mesh megakernel: one persistent grid drains `totalItems` (pixel, frame) samples of the band's
 // rows and frames [firstFrame, firstFrame+frames).
 struct MeshParams {
@@ -74,18 +85,13 @@ struct MeshParams {
     // unless the camera is a pinhole at a nonzero origin (every ray starts at cam.origin), o.xyz
     unsigned poolOffset;
     int poolWords;
+    // the previous batch's running average + tonemap, done by this launch's waves between their
+    // paths (its scratch is the other buffer): comb.bandPixels == 0 for none; chunks of 64 pixels
+    // claimed from *combCtr (zeroed with the work queue)
+    CombineParams comb;
+    unsigned *combCtr;
 };
 
-// Running average + tonemap over a batch of per-sample radiances
-// (CudaPathTracerKernel.cu:157-178).
-struct CombineParams {
-    float4 *accum;
-    uint32_t *out;
-    const float *scratch;
-    unsigned bandPixels, totalItems;
-    int firstFrame, frames;
-    int format;  // kPixelArgb / kPixelRgba8
-};
 
 // Material kinds (RayTracer.h:473-540) and the sphere flag of a shading record.
 enum { kLambertian = 0, kMetal = 1, kDielectric = 2 };

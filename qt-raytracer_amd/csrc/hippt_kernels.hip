@@ -196,6 +196,40 @@ __device__ unsigned long long g_timeline[65536 * 6];
 #ifndef HIPPT_WIDE_WAVES_PER_EU
 #define HIPPT_WIDE_WAVES_PER_EU 7
 #endif
+// Running average in frame order, then the output word (CudaPathTracerKernel.cu:157-178), of band
+// pixel p over a batch of per-sample radiances.
+template <int UNROLL>
+__device__ __forceinline__ void combine_pixel(const CombineParams &P, unsigned p) {
+    float4 acc = P.accum[p];
+#pragma unroll UNROLL
+    for (int fl = 0; fl < P.frames; ++fl) {
+        const size_t k = size_t(fl) * P.bandPixels + p;
+        const int f = P.firstFrame + fl;
+        const float ff = float(f), fc = float(f + 1);
+        const float3 L = *reinterpret_cast<const float3 *>(P.scratch + 3 * k);
+        acc.x = fmaf(acc.x, ff, L.x) / fc;
+        acc.y = fmaf(acc.y, ff, L.y) / fc;
+        acc.z = fmaf(acc.z, ff, L.z) / fc;
+    }
+    acc.w = 1.0f;
+    P.accum[p] = acc;
+    P.out[p] = pack_pixel(acc.x, acc.y, acc.z, P.format);
+}
+
+// One 64-pixel chunk of the previous batch's combine (MeshParams::comb) for the whole wave; false
+// once every chunk is claimed.  Wave-uniform.  The frame loop is not unrolled here: unrolled 8x
+// at the kernel's two call sites it cost blob70k 3% even with the combine off (r3g/r3h; none
+// without the unroll, r3i).
+__device__ __forceinline__ bool combine_chunk(const MeshParams &P) {
+    unsigned base = 0;
+    if (__lane_id() == 0) base = atomicAdd(P.combCtr, 64u);
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (base >= P.comb.bandPixels) return false;
+    const unsigned p = base + __lane_id();
+    if (p < P.comb.bandPixels) combine_pixel<1>(P.comb, p);
+    return true;
+}
+
 // Camera-ray pool (POOL, HIPPT_OPT_CAMERA_POOL): a refill happens when a lane's path ends, so only
 // the lanes whose paths ended together generate camera rays, at ~30% SIMD efficiency (Cornell,
 // tools/phase_profile.py).  With the pool, the wave generates the camera rays of its next 64 work
@@ -305,6 +339,13 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     unsigned long long nvis = 0, ntest = 0;
     unsigned pc[kProfSlots] = {0};
 
+    // The previous batch's combine (memory-bound) beside this batch's paths (VALU-bound): one wave
+    // in 8 starts with it while the others trace, and every wave takes what is left when its
+    // paths run out (the launch's tail, where the traversal leaves SIMDs idle).  Not inside the
+    // path loop: with the paths' state live it costs registers.
+    bool combLeft = P.comb.bandPixels != 0;
+    if (combLeft && (blockIdx.x & 1u) == 0 && threadIdx.x < 64u)
+        while (combLeft) combLeft = combine_chunk(P);
     for (;;) {
         prof<STATS>(pc, 0);
         // ---- refill: every lane whose sample ended takes the next (pixel, frame) -------------
@@ -436,6 +477,8 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         }
     }
 
+    while (combLeft) combLeft = combine_chunk(P);
+
 #ifdef HIPPT_DEBUG_TIMELINE
     if (__lane_id() == 0 && tlw < 65536) {
         g_timeline[6 * tlw + 1] = tlDrained;
@@ -468,21 +511,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
 // Running average in frame order, then ARGB (CudaPathTracerKernel.cu:157-178).
 __global__ __launch_bounds__(256) void combine_kernel(CombineParams P) {
     const unsigned stride = gridDim.x * 256u;
-    for (unsigned p = blockIdx.x * 256u + threadIdx.x; p < P.bandPixels; p += stride) {
-        float4 acc = P.accum[p];
-        for (int fl = 0; fl < P.frames; ++fl) {
-            const size_t k = size_t(fl) * P.bandPixels + p;
-            const int f = P.firstFrame + fl;
-            const float ff = float(f), fc = float(f + 1);
-            const float3 L = *reinterpret_cast<const float3 *>(P.scratch + 3 * k);
-            acc.x = fmaf(acc.x, ff, L.x) / fc;
-            acc.y = fmaf(acc.y, ff, L.y) / fc;
-            acc.z = fmaf(acc.z, ff, L.z) / fc;
-        }
-        acc.w = 1.0f;
-        P.accum[p] = acc;
-        P.out[p] = pack_pixel(acc.x, acc.y, acc.z, P.format);
-    }
+    for (unsigned p = blockIdx.x * 256u + threadIdx.x; p < P.bandPixels; p += stride) combine_pixel<8>(P, p);
 }
 
 // table[s] for s = 0 .. 2^32-1: the state from which random_in_unit_sphere, entered with state s,

@@ -30,7 +30,7 @@ def pt():
                  (hippt.OPT_STACK_CAP, 0), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_LDS_TOP_NODES, -1),
                  (hippt.OPT_RNG_TABLE, 0), (hippt.OPT_BVH_COLLAPSE, 0), (hippt.OPT_BVH_NODE_COST, 200),
                  (hippt.OPT_BVH_LEAF4, 4), (hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_ARGB),
-                 (hippt.OPT_CAMERA_POOL, -1)):
+                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1)):
         t.setOption(k, v)
     t.resetStats()
     yield t
@@ -483,6 +483,66 @@ def test_mesh_batches_and_frame_splits_are_bit_identical(pt):
         assert pt.renderFrames(n, 8)
     split = pt.readback()
     _assert_same(one[0], one[1], split[0], split[1])
+
+
+@pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene"])
+def test_deferred_combine_across_async_calls(pt, name):
+    """Back-to-back hipptRenderFramesAsync calls: each megakernel batch's combine (running average
+    + tonemap) runs inside the next batch's launch (Ctx::deferred), from the other scratch buffer;
+    anything that reads or resets the image runs the pending one first.  Every sequence below
+    gives the oracle's progressive image bit for bit."""
+    sc = scenes.get_scene(name)
+    w, h = 45, 26
+    ora6 = po.MeshScene(sc, w, h).frames(0, 6, 8)
+    pt.uploadMesh(sc)
+    # fused off: every batch's combine its own launch
+    pt.setOption(hippt.OPT_FUSE_COMBINE, 0)
+    assert pt.initialize(w, h)
+    for _ in range(6):
+        assert pt.renderFramesAsync(1, 8), pt.lastError()
+    got = pt.readback()
+    _assert_same(got[0], got[1], ora6[0], ora6[1])
+    pt.setOption(hippt.OPT_FUSE_COMBINE, -1)
+    # one frame per call: a chain of five deferred combines, the last one run by readback's sync
+    assert pt.initialize(w, h)
+    for _ in range(6):
+        assert pt.renderFramesAsync(1, 8), pt.lastError()
+    got = pt.readback()
+    _assert_same(got[0], got[1], ora6[0], ora6[1])
+    # several batches per call (tiny scratch cap): deferred within the call as well
+    pt.setOption(hippt.OPT_SCRATCH_MB, 1)
+    assert pt.initialize(w, h)
+    assert pt.renderFramesAsync(4, 8) and pt.renderFramesAsync(2, 8)
+    got = pt.readback()
+    _assert_same(got[0], got[1], ora6[0], ora6[1])
+    pt.setOption(hippt.OPT_SCRATCH_MB, 32768)
+    # a reset between async calls runs the pending combine first, then clears the accumulation
+    assert pt.initialize(w, h)
+    assert pt.renderFramesAsync(3, 8)
+    assert pt.resetAccumulation()
+    for _ in range(6):
+        assert pt.renderFramesAsync(1, 8)
+    got = pt.readback()
+    _assert_same(got[0], got[1], ora6[0], ora6[1])
+    # a wavefront batch after megakernel batches flushes their combine before its own
+    assert pt.initialize(w, h)
+    assert pt.renderFramesAsync(2, 8)
+    pt.setOption(hippt.OPT_PATH_MODE, 1)
+    assert pt.renderFramesAsync(2, 8)
+    pt.setOption(hippt.OPT_PATH_MODE, 0)
+    assert pt.renderFramesAsync(2, 8)
+    got = pt.readback()
+    _assert_same(got[0], got[1], ora6[0], ora6[1])
+    # the present hand-off and a blocking render see finished images
+    assert pt.initialize(w, h)
+    assert pt.renderFramesAsync(3, 8)
+    assert pt.renderFramesPresent(3, 8)
+    assert pt.synchronize()
+    img, frames = pt.latestFrame()
+    assert frames == 6 and np.array_equal(img, ora6[0])
+    assert pt.initialize(w, h)
+    assert pt.renderFramesAsync(5, 8) and pt.renderFrames(1, 8)
+    assert np.array_equal(pt.hostPixels(), ora6[0])
 
 
 def test_mesh_row_range_and_two_contexts(pt):
