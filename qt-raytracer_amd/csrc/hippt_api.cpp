@@ -548,13 +548,18 @@ bool run_wavefront(Ctx &c, hippt::MeshParams p, bool cnt, bool spills, int spill
     for (hipEvent_t &e : c.wfPoll)
         if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     int cur = 0;
+    // A pool that holds every work item of the batch generates them all up front and never
+    // regenerates, and every path ends within maxDepth extend rounds: exactly maxDepth iterations,
+    // no polling (a polled loop runs up to 2*kPollEvery - 1 empty iterations past the end).
+    const bool allInFlight = slots >= p.totalItems;
     for (long long it = 0;; ++it) {
+        if (allInFlight && it == p.maxDepth) break;
         if (it > maxIter) return fail(err, "wavefront path tracer did not drain its ray queue");
         HIP_TRY(hippt::wf_launch_extend(W, cur, blocks, cnt, c.stream));
         HIP_TRY(hippt::wf_launch_shade(W, cur, c.stream));
-        HIP_TRY(hippt::wf_launch_generate(W, cur ^ 1, true, c.stream));
+        HIP_TRY(hippt::wf_launch_generate(W, cur ^ 1, true, c.stream, allInFlight));
         cur ^= 1;
-        if (it % kPollEvery != kPollEvery - 1) continue;
+        if (allInFlight || it % kPollEvery != kPollEvery - 1) continue;
         const int b = int(it / kPollEvery) & 1;
         HIP_TRY(hipMemcpyAsync(c.wfHost + b * kSnap, c.wfCtr + hippt::ctr_word(hippt::kCtrExt0 + cur * hippt::kWfShards),
                                kSnap * sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));

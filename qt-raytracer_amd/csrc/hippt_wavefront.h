@@ -45,7 +45,9 @@ struct WfParams {
 size_t wf_pool_words(unsigned slots, unsigned *shardCap);
 hipError_t wf_launch_init(const WfParams &W, hipStream_t s);
 // countSamples: the regenerate queue holds finished samples (false for the initial fill).
-hipError_t wf_launch_generate(const WfParams &W, int nxt, bool countSamples, hipStream_t s);
+// countOnly: nothing is left to generate (every work item of the batch was generated up front);
+// one block per shard only counts the finished samples
+hipError_t wf_launch_generate(const WfParams &W, int nxt, bool countSamples, hipStream_t s, bool countOnly = false);
 hipError_t wf_launch_extend(const WfParams &W, int cur, int blocks, bool countTraversal, hipStream_t s);
 hipError_t wf_launch_shade(const WfParams &W, int cur, hipStream_t s);
 int wf_extend_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,

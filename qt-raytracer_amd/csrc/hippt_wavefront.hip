@@ -211,10 +211,15 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(WfParams W, int cur) {
     const MeshParams &P = W.mp;
     if (blockIdx.x == 0 && threadIdx.x < kWfShards) W.ctr[ctr_word(kCtrFetch + int(threadIdx.x))] = 0;
     const unsigned shard = blockIdx.x % kWfShards;
-    const unsigned local = (blockIdx.x / kWfShards) * kWfBlock + threadIdx.x;
+    const unsigned first = (blockIdx.x / kWfShards) * kWfBlock;
+    const unsigned count = W.ctr[ctr_word(kCtrExt0 + cur * kWfShards + int(shard))];
+    // the grid covers a full shard; blocks past this iteration's queue leave before the appends
+    // (block-uniform: no thread of such a block appends, so none needs the barriers)
+    if (first >= count) return;
+    const unsigned local = first + threadIdx.x;
     bool again = false, finished = false;
     unsigned slot = kNone;
-    if (local < W.ctr[ctr_word(kCtrExt0 + cur * kWfShards + int(shard))]) {
+    if (local < count) {
         slot = (cur ? W.extQ1 : W.extQ0)[shard * W.shardCap + local];
         const float4 *p = W.st + 4 * size_t(slot);
         const float4 a = p[0], b = p[1], c = p[2], h = p[3];
@@ -272,6 +277,9 @@ __global__ __launch_bounds__(kWfBlock) void wf_generate(WfParams W, int nxt, int
         }
     }
     const unsigned base = W.ctr[ctr_word(kCtrWork)];  // advanced by the next wf_extend
+    // blocks with nothing to generate leave before the appends (block-uniform, see wf_shade)
+    const unsigned first = local - threadIdx.x;
+    if (first >= here || base + lower + first >= P.totalItems) return;
     const bool ok = local < here && base + lower + local < P.totalItems;
     unsigned slot = kNone;
     if (ok) {
@@ -317,8 +325,8 @@ hipError_t wf_launch_init(const WfParams &W, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t wf_launch_generate(const WfParams &W, int nxt, bool countSamples, hipStream_t s) {
-    hipLaunchKernelGGL(wf_generate, dim3(shard_grid(W)), dim3(kWfBlock), 0, s, W, nxt,
+hipError_t wf_launch_generate(const WfParams &W, int nxt, bool countSamples, hipStream_t s, bool countOnly) {
+    hipLaunchKernelGGL(wf_generate, dim3(countOnly ? unsigned(kWfShards) : shard_grid(W)), dim3(kWfBlock), 0, s, W, nxt,
                        countSamples ? 1 : 0);
     return hipGetLastError();
 }
