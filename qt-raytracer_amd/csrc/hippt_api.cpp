@@ -549,8 +549,9 @@ bool run_wavefront(Ctx &c, hippt::MeshParams p, bool cnt, bool spills, int spill
         if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     int cur = 0;
     // A pool that holds every work item of the batch generates them all up front and never
-    // regenerates, and every path ends within maxDepth extend rounds: exactly maxDepth iterations,
-    // no polling (a polled loop runs up to 2*kPollEvery - 1 empty iterations past the end).
+    // regenerates, and every path ends within maxDepth extend rounds: at most maxDepth iterations
+    // (a polled loop alone runs up to 2*kPollEvery - 1 empty iterations past the end; the poll
+    // still ends a deep maxDepth early once every path has ended).
     const bool allInFlight = slots >= p.totalItems;
     for (long long it = 0;; ++it) {
         if (allInFlight && it == p.maxDepth) break;
@@ -559,7 +560,7 @@ bool run_wavefront(Ctx &c, hippt::MeshParams p, bool cnt, bool spills, int spill
         HIP_TRY(hippt::wf_launch_shade(W, cur, c.stream));
         HIP_TRY(hippt::wf_launch_generate(W, cur ^ 1, true, c.stream, allInFlight));
         cur ^= 1;
-        if (allInFlight || it % kPollEvery != kPollEvery - 1) continue;
+        if (it % kPollEvery != kPollEvery - 1) continue;
         const int b = int(it / kPollEvery) & 1;
         HIP_TRY(hipMemcpyAsync(c.wfHost + b * kSnap, c.wfCtr + hippt::ctr_word(hippt::kCtrExt0 + cur * hippt::kWfShards),
                                kSnap * sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));

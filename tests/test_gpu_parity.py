@@ -111,11 +111,15 @@ def test_mesh_matches_oracle(pt, name, w, h, spp, depth):
     ("blob70k", 64, 48, 4, 8, 1000, 0, 0),
     ("blob70k", 64, 48, 4, 8, 5000, 0, 6),
     ("blob70k", 20, 11, 2, 1, 100, 2, 0),
+    ("cornell34", 40, 30, 4, 50, 1 << 20, 0, 0),
+    ("blob70k", 32, 24, 3, 1, 1 << 20, 0, 0),
 ])
 def test_wavefront_matches_oracle(pt, name, w, h, spp, depth, slots, width, cap):
     """The wavefront variant (BASELINE config 5) is bit-identical to the oracle/megakernel,
     including with a path pool much smaller than the work (many regenerate rounds), over the
-    2-wide and the 4-wide trees (a small LDS stack cap forces spills to the global area)."""
+    2-wide and the 4-wide trees (a small LDS stack cap forces spills to the global area), and
+    with a pool that holds the whole batch (at most maxDepth iterations, the queue poll ending a
+    deep maxDepth early)."""
     sc = scenes.get_scene(name)
     pt.uploadMesh(sc)
     pt.setOption(hippt.OPT_PATH_MODE, 1)
