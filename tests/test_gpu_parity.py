@@ -88,6 +88,7 @@ def test_legacy_depth_edge_cases(pt, depth):
 
 # ---- triangle meshes -------------------------------------------------------------------------------
 @pytest.mark.parametrize("name,w,h,spp,depth", [
+    ("cornell34", 256, 256, 4, 4),  # BASELINE configs[0] (the CPU plumbing/parity case), whole image
     ("cornell34", 96, 64, 8, 8),
     ("cornell34", 33, 17, 3, 4),
     ("blob70k", 64, 48, 4, 8),
