@@ -187,7 +187,7 @@ enum {
     HIPPT_OPT_LDS_SCENE = 6,        /* 1 (default): small scenes are copied into LDS per block */
     HIPPT_OPT_PATH_MODE = 8,        /* 0 (default): persistent megakernel; 1: wavefront kernels */
     HIPPT_OPT_WAVEFRONT_SLOTS = 9,  /* wavefront path-state slots per device, 64..2^28 (default 2^27) */
-    HIPPT_OPT_BVH_LEAF = 10,        /* max primitives per BVH leaf, 1..15; applies at the next upload */
+    HIPPT_OPT_BVH_LEAF = 10,        /* max primitives per BVH leaf, 1..15 (default 2); applies at the next upload */
     HIPPT_OPT_BVH_TRAVERSAL_COST = 11, /* SAH node-step cost in 1/100 primitive tests; next upload */
     HIPPT_OPT_BVH_MAX_DEPTH = 12,   /* interior-level bound (LDS stack per lane), 1..32; next upload */
     HIPPT_OPT_DEVICE_ROWS = 13,     /* hipptSetDevices split: 1 (default) interleaved rows, 0 bands; next Init */

@@ -15,7 +15,10 @@ namespace hippt {
 // Stack entries the kernel keeps per lane in LDS; the builder guarantees that no
 // traversal needs more (interior levels <= kStackDepth).
 constexpr int kStackDepth = 32;
-constexpr int kMaxLeafTris = 4;
+// Default leaf size: 2 primitives (r3ag, alternating A/B on the final kernels: blob70k +1.3%, Cornell
+// +1.1%, random_scene +0.3%, cornell_mixed +0.2% over 4; the 4-wide collapse leaves visit and test
+// counts nearly unchanged, the leaf loop's per-lane trip counts less uneven).
+constexpr int kMaxLeafTris = 2;
 constexpr int kNodeWords = 16;  // 64 B: two child boxes + two child codes
 
 // Build parameters: SAH with a traversal step costing `traversalCost` primitive tests, leaves of
