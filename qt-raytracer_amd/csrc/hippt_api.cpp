@@ -41,7 +41,9 @@ constexpr int kStatWords = 32;  // [0..3] hipptStats counters, [4..19] phase pro
 // 4-wide traversal: LDS stack content capacity for scenes outside LDS (19 + 3 spare entries =
 // 22 KB per 256-lane block: 7 blocks per CU in 160 KB).
 constexpr int kWideStackCap = 19;
-constexpr int kSpillStackCap = 13;
+// a tree that spills anyway keeps 10 entries and gives the rest to the top of the tree (r3al,
+// alternating on leaf-2 trees: blob70k 1080p +0.5%, 4K +0.6% over 13; r3q before: +0.6%)
+constexpr int kSpillStackCap = 10;
 // 4-wide trees are numbered breadth-first for their first kTopOrderNodes nodes, so that a prefix
 // of the node array is the top of the tree; trees read from global memory keep such a prefix in
 // LDS (HIPPT_OPT_LDS_TOP_NODES)
@@ -676,7 +678,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 // traversal of a tree in global memory whose bound exceeds kWideStackCap (it
                 // spills anyway) keeps kSpillStackCap entries and gives the rest of its LDS to the
                 // top of the tree (blob70k, float nodes: cap 19 + 4 top nodes 17.8 G, cap 13 + 52
-                // top nodes 20.4 G; caps 9-15 within 1%, 7: -3%; r2w)
+                // top nodes 20.4 G; caps 9-15 within 1%, 7: -3%; r2w; cap 10 + 76 nodes +0.5%, r3al)
                 const bool topTree = wide && !ldsScene;
                 const int capLimit = s.stackCap > 0 ? s.stackCap
                                      : ldsScene     ? 30
