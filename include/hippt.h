@@ -212,7 +212,9 @@ enum {
                                        there; 0: none; -1 (default): automatic (what the LDS budget of the
                                        resident blocks leaves beside the stack) */
     , HIPPT_OPT_BVH_COLLAPSE = 21   /* 2-wide -> 4-wide collapse: 0 greedy (open the largest child), 1 SAH-optimal
-                                       (dynamic programming); next upload */
+                                       (dynamic programming), -1 (default) SAH-optimal for scenes that fit
+                                       the LDS scene copy, else greedy; next upload (hipptBvhBuild: -1 =
+                                       greedy) */
     , HIPPT_OPT_BVH_NODE_COST = 22  /* SAH-optimal collapse: a 4-wide node visit in 1/100 primitive tests; next upload */
     , HIPPT_OPT_BVH_LEAF4 = 23      /* SAH-optimal collapse: most primitives per 4-wide leaf, 1..15; next upload */
     , HIPPT_OPT_RNG_TABLE = 24      /* 1: random_in_unit_sphere's rejection loop as one lookup in a 16 GiB

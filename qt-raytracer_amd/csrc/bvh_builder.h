@@ -32,8 +32,10 @@ struct BvhParams {
     int sahMode = 1;  // 0: 16 bins on the longest centroid axis; 1: all axes, exact sweep (32 bins on big nodes)
     // 4-wide collapse: 0 opens the largest-area interior child until a node has 4 children; 1 the
     // SAH-optimal collapse (nodeCost = a 4-wide node visit in primitive tests; leaves may merge
-    // 2-wide subtrees up to maxLeaf4 primitives)
-    int collapse = 0;
+    // 2-wide subtrees up to maxLeaf4 primitives); -1 automatic: the scene upload takes the
+    // SAH-optimal tree when the scene fits the LDS scene copy, else greedy (collapse_bvh4 itself
+    // treats -1 as greedy)
+    int collapse = -1;
     float nodeCost = 2.0f;
     int maxLeaf4 = 4;
 };

@@ -963,6 +963,22 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
     std::memcpy(sc.nodes.data(), bvh.nodes.data(), bvh.nodes.size() * sizeof(uint32_t));
     hippt::Bvh4 bvh4;
     hippt::collapse_bvh4(bvh, bvh4, s.bvh);
+    if (s.bvh.collapse == -1) {
+        // Automatic collapse: the SAH-optimal 4-wide tree for scenes that fit the LDS scene copy
+        // (leaves of <= 2 primitives: Cornell +1.6-1.9%, cornell_mixed +1.0%, r3ap/r3aq), the
+        // greedy one for trees read from global memory (SAH-optimal: blob70k -9%, random_scene -4%)
+        auto fits = [&](const hippt::Bvh4 &b) {
+            return hippt::mesh_lds_bytes(0, int(b.nodes.size() / hippt::kNode4Words), numPrims, true, 0,
+                                         numMaterials) <= hippt::mesh_lds_scene_limit();
+        };
+        if (fits(bvh4)) {
+            hippt::BvhParams p = s.bvh;
+            p.collapse = 1;
+            hippt::Bvh4 sah;
+            hippt::collapse_bvh4(bvh, sah, p);
+            if (fits(sah)) bvh4 = std::move(sah);
+        }
+    }
     hippt::order_bvh4_top(bvh4, kTopOrderNodes);
     sc.nodes4.assign(bvh4.nodes.size() / 4, float4{});
     std::memcpy(sc.nodes4.data(), bvh4.nodes.data(), bvh4.nodes.size() * sizeof(uint32_t));
@@ -1368,7 +1384,7 @@ extern "C" bool hipptSetOption(int key, long long value) {
         s.ldsTopNodes = int(value);
         return true;
     case HIPPT_OPT_BVH_COLLAPSE:
-        if (value != 0 && value != 1) return false;
+        if (value < -1 || value > 1) return false;
         s.bvh.collapse = int(value);
         return true;
     case HIPPT_OPT_BVH_NODE_COST:

@@ -82,7 +82,7 @@ def test_options_validate():
 
 @pytest.mark.parametrize("key,good,bad,default", [
     (hippt.OPT_LDS_TOP_NODES, (0, 1, 85, 1365), (-2, 1366), -1),
-    (hippt.OPT_BVH_COLLAPSE, (0, 1), (-1, 2), 0),
+    (hippt.OPT_BVH_COLLAPSE, (-1, 0, 1), (-2, 2), -1),
     (hippt.OPT_BVH_NODE_COST, (1, 250, 100000), (0, 100001), 200),
     (hippt.OPT_BVH_LEAF4, (1, 8, 15), (0, 16), 4),
     (hippt.OPT_RNG_TABLE, (0, 1), (-1, 2), 0),

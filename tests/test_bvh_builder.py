@@ -166,7 +166,7 @@ def test_bvh4_sah_collapse_partitions_primitives(name, leaf4):
         assert lib.hipptSetOption(hippt.OPT_BVH_COLLAPSE, 1) and lib.hipptSetOption(hippt.OPT_BVH_LEAF4, leaf4)
         bvh = hippt.Bvh(sc.verts, extent_hint=800.0)
     finally:
-        lib.hipptSetOption(hippt.OPT_BVH_COLLAPSE, 0)
+        lib.hipptSetOption(hippt.OPT_BVH_COLLAPSE, -1)
         lib.hipptSetOption(hippt.OPT_BVH_LEAF4, 4)
     f, kids = _decode4(bvh.nodes4)
     covered = np.zeros(sc.num_tris, np.int32)
