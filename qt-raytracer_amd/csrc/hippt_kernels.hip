@@ -193,6 +193,13 @@ __device__ unsigned long long g_timeline[65536 * 6];
 #endif
 #define HIPPT_SGPR_ATTR __attribute__((amdgpu_num_sgpr(HIPPT_NUM_SGPR)))
 
+// Lambertian-triangle kernels: a shading pass runs at most this many tries of the unit-sphere
+// draw; a lane whose draw is still rejecting stays on its hit and resumes the same chain in the
+// next pass (0: the whole draw in one pass).
+#ifndef HIPPT_REJECT_CAP
+#define HIPPT_REJECT_CAP 0
+#endif
+
 #ifndef HIPPT_WIDE_WAVES_PER_EU
 #define HIPPT_WIDE_WAVES_PER_EU 7
 #endif
@@ -333,6 +340,8 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     T.bestO = 0x7fffffff;
     float tr = 1, tg = 1, tb = 1;
     bool need = true, fresh = false;
+    constexpr unsigned CAP = FULL ? 0u : unsigned(HIPPT_REJECT_CAP);
+    unsigned pend = 0;  // tries so far of a pending unit-sphere draw (CAP), 0 = none
     // per-lane counts fit 32 bits (a lane traces a few thousand segments per launch); widened
     // for the wave sum
     unsigned segs = 0, samples = 0;
@@ -423,10 +432,10 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
             prepare(r);
             begin(T);
         }
-        if (!__any(busy(T))) break;
+        if (!__any(busy(T) || pend != 0u)) break;
 
         // ---- traversal: while-while over the BVH; leave once few lanes remain -------------
-        do {
+        if (!CAP || __any(busy(T))) do {
             prof<STATS>(pc, 2);
             if (WIDE)
                 traverse_round_wide<nodeF4, STATS, FULL, QUANT, SPILL, LDS_SCENE, TOP>(
@@ -438,21 +447,34 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         // ---- shading: lanes whose traversal finished (ray_color step, RayTracer.h:579-596) ----
         if (item != kNone && !busy(T)) {
             prof<STATS>(pc, 6);
-            ++segs;
+            const bool cont = CAP && pend != 0u;  // resumes a pending draw: same segment
+            if (!cont) ++segs;
             bool finished = false;
             float Lr = 0.0f, Lg = 0.0f, Lb = 0.0f;
             if (!FULL) {
                 // Lambertian triangles: the sky's 1/sqrt(|d|^2) and the scatter's 1/sqrt(|q|^2) as one
                 // sequence for both kinds of lanes (the draw first: no other draw precedes it)
-                const bool miss = T.bestI < 0;
+                const bool miss = !cont && T.bestI < 0;
                 // depth exhausted: contributes 0 (RayTracer.h:582-583)
-                const bool scat = !miss && ++depth < P.maxDepth;
+                const bool scat = cont || (!miss && ++depth < P.maxDepth);
                 float qx = 0.0f, qy = 0.0f, qz = 0.0f;
                 float x = fdot(r.dx, r.dy, r.dz, r.dx, r.dy, r.dz);
-                if (scat) x = rius<STATS>(rng, qx, qy, qz, pc, P.rngTable);
+                bool drawn = true;
+                if (scat) {
+                    if (CAP && !P.rngTable) {
+                        const float q2 = rius_capped<STATS>(rng, qx, qy, qz, pend, CAP, pc);
+                        drawn = q2 >= 0.0f;
+                        if (drawn) {
+                            x = q2;
+                            pend = 0;
+                        }
+                    } else {
+                        x = rius<STATS>(rng, qx, qy, qz, pc, P.rngTable);
+                    }
+                }
                 const float inv = rsqrt_rn(x);
                 if (miss) sky_inv(r, inv, tr, tg, tb, Lr, Lg, Lb);
-                if (scat) {
+                if (scat && drawn) {
                     lambert_apply(r, T.bestT, T.bestI, shade, mats, qx, qy, qz, inv, tr, tg, tb);
                     fresh = true;
                 }

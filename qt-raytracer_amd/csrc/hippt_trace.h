@@ -341,6 +341,25 @@ __device__ __forceinline__ float rius(uint32_t &rng, float &rx, float &ry, float
     return r2;
 }
 
+// The same draw in at most `cap` tries per call: `tries` (persistent, 0 before the first try)
+// continues the lane's chain across calls, so the draws and the escape points are rius's.
+// Returns |p|^2 once a candidate is accepted, -1 while the draw is still pending.
+template <bool STATS>
+__device__ __forceinline__ float rius_capped(uint32_t &rng, float &rx, float &ry, float &rz, unsigned &tries,
+                                             unsigned cap, unsigned *pc) {
+    for (unsigned k = 0; k < cap; ++k) {
+        prof<STATS>(pc, 7);
+        rx = rand_pm1(rng);
+        ry = rand_pm1(rng);
+        rz = rand_pm1(rng);
+        const float r2 = fmaf(rx, rx, fmaf(ry, ry, rz * rz));
+        ++tries;
+        if (r2 < 1.0f) return r2;
+        escape_cycle(rng, tries);
+    }
+    return -1.0f;
+}
+
 // Scatter at the closest hit (ray_color :585-590 + the material's scatter, :473-540) of
 // primitive `prim` at t.  The ray becomes the scattered ray and the throughput takes the
 // attenuation; false = absorbed (Metal below the surface), which contributes 0.  FULL=false
