@@ -274,6 +274,9 @@ void hipptBvh4Copy(const hipptBvh *bvh, uint32_t *nodes);
  * child i, plane = origin + byte * scale); scale y; scale z; child[4].  Every decoded box
  * contains the float box of hipptBvh4Copy; an unused slot has lo bytes 255 and hi bytes 0. */
 void hipptBvh4QCopy(const hipptBvh *bvh, uint32_t *nodes);
+/* Nodes of that 8-bit tree: Bvh4NodeCount, or 0 when the scene has none (boxes near +-FLT_MAX,
+ * which no finite grid covers; the kernels then read the float nodes). */
+int hipptBvh4QNodeCount(const hipptBvh *bvh);
 
 #ifdef __cplusplus
 }

@@ -607,7 +607,7 @@ int order_bvh4_top(Bvh4 &b, int topNodes) {
     return int(bfs.size());
 }
 
-void quantize_bvh4(const Bvh4 &in, std::vector<uint32_t> &out) {
+bool quantize_bvh4(const Bvh4 &in, std::vector<uint32_t> &out) {
     const size_t n = in.nodes.size() / kNode4Words;
     out.assign(n * kNode4QWords, 0u);
     const int32_t unused = leaf_code(0, 0);
@@ -628,12 +628,21 @@ void quantize_bvh4(const Bvh4 &in, std::vector<uint32_t> &out) {
                     hi = std::max(hi, f[8 * a + 4 + i]);
                 }
             if (!(lo <= hi)) lo = hi = 0.0f;  // no used child (never built; kept total)
+            if (!std::isfinite(lo) || !std::isfinite(hi)) {  // padded past FLT_MAX
+                out.clear();
+                return false;
+            }
             // Smallest power-of-two scale s whose grid, with its origin at least one step below
-            // lo, covers [lo, hi] with every plane at least one step outside: a plane is moved
-            // one more step outward when it falls exactly on the grid, so the decoded plane
-            // stays outside the float plane even after the kernel's three roundings of
-            // q*(s*inv) + (o*inv - o_ray*inv) (the float path rounds once).  The differences
-            // are exact in double, the division by s too.
+            // lo, covers [lo, hi] with every plane at least one step outside (a plane on the grid
+            // moves one more step out): every decoded plane lies outside the Bvh4 plane, which
+            // the builder already padded by M * 2^-16 (M = the largest |coordinate| of any
+            // primitive or the camera, bvh_builder.cpp build_bvh_boxes).  That global pad, not
+            // the grid step, is what absorbs the kernel's roundings of q*(s*inv) +
+            // (o*inv - o_ray*inv): each of its three roundings errs by at most 2^-24 of a term
+            // bounded by M*|inv| (|o| and |o_ray| are at most ~M: ray origins are points on
+            // primitives or the camera), about 2^-21 * M * |inv| in all, 2^5 times below the pad
+            // even for a node far smaller than its distance from the ray origin.  The
+            // differences are exact in double, the division by s too.
             const double ext = double(hi) - double(lo);
             int e = -100;
             if (ext > 0) {
@@ -644,8 +653,18 @@ void quantize_bvh4(const Bvh4 &in, std::vector<uint32_t> &out) {
             uint32_t ql[4], qh[4];
             float o = lo;
             for (;; ++e) {
+                // boxes near +-FLT_MAX: no finite grid (origin or scale overflows) covers them;
+                // the scene then has no 8-bit tree (the kernels use the float nodes)
+                if (e > 126) {
+                    out.clear();
+                    return false;
+                }
                 const double s = std::ldexp(1.0, e);
                 o = float(double(lo) - s);
+                if (!std::isfinite(o)) {
+                    out.clear();
+                    return false;
+                }
                 if (double(o) > double(lo) - s) o = std::nextafter(o, -INFINITY);  // round down
                 bool fits = true;
                 for (int i = 0; i < 4 && fits; ++i) {
@@ -680,6 +699,7 @@ void quantize_bvh4(const Bvh4 &in, std::vector<uint32_t> &out) {
         std::memcpy(&d[11], &scale[2], sizeof(float));
         for (int i = 0; i < 4; ++i) d[12 + i] = w[24 + i];
     }
+    return true;
 }
 
 }  // namespace hippt

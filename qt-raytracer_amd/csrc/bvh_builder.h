@@ -87,7 +87,9 @@ int order_bvh4_top(Bvh4 &b, int topNodes);
 // Planes are rounded outward (lo down, hi up), so every decoded box contains the Bvh4 box (which
 // is already padded for the kernel's slab-test rounding).  An unused child slot has lo = 255,
 // hi = 0 on every axis: read as near/far planes by the ray's octant it is always missed.
+// Returns false (and leaves `out` empty) for trees with boxes near +-FLT_MAX, which no finite
+// grid covers: such scenes have no 8-bit tree.
 constexpr int kNode4QWords = 16;
-void quantize_bvh4(const Bvh4 &in, std::vector<uint32_t> &out);
+bool quantize_bvh4(const Bvh4 &in, std::vector<uint32_t> &out);
 
 }  // namespace hippt

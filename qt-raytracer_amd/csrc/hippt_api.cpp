@@ -642,6 +642,8 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
         const unsigned bandPixels = unsigned(rows) * unsigned(s.width);
         if (rows > 0 && count > 0) {
             if (!mesh) {
+                // the legacy kernel writes accum/out itself: a mesh batch's pending combine goes first
+                if (!flush_deferred(c, err)) return false;
                 hippt::Sphere4Params p{c.accum, c.out, c.stats, s.width, s.height, c.y0, rows, c.stride, firstFrame, count,
                                        maxDepth, s.pixelFormat};
                 EventPair ev;
@@ -692,7 +694,8 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 // 84%, 15.6 -> 17.7 G).  Automatic for the wavefront's Lambertian-triangle kernel
                 // only: the megakernel reads the top of the tree (62-70% of the visits) from LDS,
                 // where the float nodes need no decode (blob70k 19.0 G 8-bit, 20.4 G float, r2v).
-                const bool quant = wide && !ldsScene &&
+                // (scenes with boxes near +-FLT_MAX have no 8-bit tree: quantize_bvh4 failed)
+                const bool quant = wide && !ldsScene && !s.scene.nodes4q.empty() &&
                                    (s.bvhQuant == 1 || (s.bvhQuant == -1 && !s.scene.full && s.pathMode == 1));
                 // The top of a global-memory tree in LDS (megakernel and wavefront extend): the
                 // breadth-first prefix of the node array that the LDS budget of the resident blocks
@@ -899,6 +902,9 @@ extern "C" void hipptBuildCamera(const double lookfrom[3], const double lookat[3
 extern "C" bool hipptUseBuiltinScene(int sceneId, const char **err) {
     std::lock_guard<std::mutex> g(S().mu);
     if (sceneId != HIPPT_SCENE_SPHERE4) return fail(err, "unknown built-in scene id");
+    // a pending mesh combine belongs to the image rendered so far: enqueue it before the switch
+    for (Ctx &c : S().ctxs)
+        if (!flush_deferred(c, err)) return false;
     S().scene.kind = HIPPT_SCENE_SPHERE4;
     return true;
 }
@@ -984,7 +990,7 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
     std::memcpy(sc.nodes4.data(), bvh4.nodes.data(), bvh4.nodes.size() * sizeof(uint32_t));
     sc.numNodes4 = int(bvh4.nodes.size() / hippt::kNode4Words);
     std::vector<uint32_t> q;
-    hippt::quantize_bvh4(bvh4, q);
+    (void)hippt::quantize_bvh4(bvh4, q);  // empty on failure: the float nodes serve every path
     sc.nodes4q.assign(q.size() / 4, float4{});
     std::memcpy(sc.nodes4q.data(), q.data(), q.size() * sizeof(uint32_t));
     if (bvh4.nodes.size() / hippt::kNode4Words >= (1u << 24)) return fail(err, "4-wide BVH too large (2^24 nodes)");
@@ -1475,7 +1481,7 @@ extern "C" hipptBvh *hipptBvhBuild(const float *verts, int numTris, float extent
     }
     hippt::collapse_bvh4(b->bvh, b->bvh4, params);
     hippt::order_bvh4_top(b->bvh4, kTopOrderNodes);
-    hippt::quantize_bvh4(b->bvh4, b->bvh4q);
+    (void)hippt::quantize_bvh4(b->bvh4, b->bvh4q);  // empty for boxes near +-FLT_MAX
     return b;
 }
 
@@ -1494,6 +1500,9 @@ extern "C" int hipptBvh4Depth(const hipptBvh *b) { return b ? b->bvh4.levels : 0
 extern "C" int hipptBvh4StackBound(const hipptBvh *b) { return b ? b->bvh4.stackBound : 0; }
 extern "C" void hipptBvh4Copy(const hipptBvh *b, uint32_t *nodes) {
     if (b && nodes) std::memcpy(nodes, b->bvh4.nodes.data(), b->bvh4.nodes.size() * sizeof(uint32_t));
+}
+extern "C" int hipptBvh4QNodeCount(const hipptBvh *b) {
+    return b ? int(b->bvh4q.size() / hippt::kNode4QWords) : 0;
 }
 extern "C" void hipptBvh4QCopy(const hipptBvh *b, uint32_t *nodes) {
     if (b && nodes) std::memcpy(nodes, b->bvh4q.data(), b->bvh4q.size() * sizeof(uint32_t));

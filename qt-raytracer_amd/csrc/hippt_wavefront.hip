@@ -342,13 +342,12 @@ hipError_t wf_launch_extend(const WfParams &W, int cur, int blocks, bool countTr
                        P.topBytes > (unsigned(P.numNodes) << (P.wide == 2 ? 6 : 7))))
         return hipErrorInvalidValue;
     const size_t bytes = mesh_lds_bytes(P.stackDepth, lds ? P.numNodes : 0, lds ? P.numTris : 0, P.wide != 0, P.topBytes);
-    if (P.wide && (lds || P.topBytes)) {
-        const hipError_t e = check_lds_at_zero(
-            reinterpret_cast<const void *>(ext_fn(countTraversal, lds, P.full != 0, P.wide != 0, false)));
+    const auto fn = ext_fn(countTraversal, lds, P.full != 0, P.wide != 0, P.wide == 2 && !lds);
+    if (P.wide && (lds || P.topBytes)) {  // the variant launched (8-bit nodes included) reads LDS at 0
+        const hipError_t e = check_lds_at_zero(reinterpret_cast<const void *>(fn));
         if (e != hipSuccess) return e;
     }
-    hipLaunchKernelGGL(ext_fn(countTraversal, lds, P.full != 0, P.wide != 0, P.wide == 2 && !lds), dim3(blocks),
-                       dim3(kMeshBlock), bytes, s, W, cur);
+    hipLaunchKernelGGL(fn, dim3(blocks), dim3(kMeshBlock), bytes, s, W, cur);
     return hipGetLastError();
 }
 

@@ -69,7 +69,7 @@ EXPORTS = (
     "hipptResetAccumulation", "hipptGetStats", "hipptResetStats", "hipptGetCounters", "hipptSetOption",
     "hipptGetOption",
     "hipptLastError", "hipptBvhBuild", "hipptBvhNodeCount", "hipptBvhDepth", "hipptBvhCopy", "hipptBvhFree",
-    "hipptBvh4NodeCount", "hipptBvh4Depth", "hipptBvh4StackBound", "hipptBvh4Copy", "hipptBvh4QCopy",
+    "hipptBvh4NodeCount", "hipptBvh4Depth", "hipptBvh4StackBound", "hipptBvh4Copy", "hipptBvh4QCopy", "hipptBvh4QNodeCount",
     "hipptActiveBvhWidth",
 )
 
@@ -176,6 +176,7 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     sig("hipptBvh4StackBound", c_int, ctypes.c_void_p)
     sig("hipptBvh4Copy", None, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32))
     sig("hipptBvh4QCopy", None, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32))
+    sig("hipptBvh4QNodeCount", c_int, ctypes.c_void_p)
     _lib = lib
     return lib
 
@@ -238,7 +239,7 @@ class Bvh:
             self.stack_bound4 = lib.hipptBvh4StackBound(h)
             self.nodes4 = np.zeros((lib.hipptBvh4NodeCount(h), 32), dtype=np.uint32)
             lib.hipptBvh4Copy(h, _ptr(self.nodes4, ctypes.c_uint32))
-            self.nodes4q = np.zeros((self.nodes4.shape[0], 16), dtype=np.uint32)
+            self.nodes4q = np.zeros((lib.hipptBvh4QNodeCount(h), 16), dtype=np.uint32)
             lib.hipptBvh4QCopy(h, _ptr(self.nodes4q, ctypes.c_uint32))
         finally:
             lib.hipptBvhFree(h)

@@ -8,10 +8,16 @@ namespace {
 // The GL / Vulkan shaders clamp the bounce count (GpuPathTracer.cpp:57, VulkanPathTracer.cpp:95)
 int clamp_depth(int maxDepth) { return std::clamp(maxDepth, 1, 64); }
 
+// A blocking render of RGBA8 words; the process-wide pixel format is restored afterwards, so other
+// hipptRenderFrames* callers in the process keep theirs (the render has combined and copied its
+// frames before it returns: nothing pending still reads the option).
 bool rgba8_frames(int first, int count, int maxDepth, const unsigned int **pixels, std::string &error) {
     const char *err = nullptr;
-    if (!hipptSetOption(HIPPT_OPT_PIXEL_FORMAT, HIPPT_PIXEL_RGBA8) ||
-        !hipptRenderFrames(first, count, maxDepth, pixels, &err)) {
+    const long long saved = hipptGetOption(HIPPT_OPT_PIXEL_FORMAT);
+    const bool ok = hipptSetOption(HIPPT_OPT_PIXEL_FORMAT, HIPPT_PIXEL_RGBA8) &&
+                    hipptRenderFrames(first, count, maxDepth, pixels, &err);
+    hipptSetOption(HIPPT_OPT_PIXEL_FORMAT, saved);
+    if (!ok) {
         error = err ? err : "HIP render failed";
         return false;
     }

@@ -136,10 +136,11 @@ int main(int argc, char **argv) {
                 }
             std::fclose(f);
         }
+        // the process-wide word format is back to its default after the RGBA8 interfaces' renders
         std::printf("{\"backend\": \"%s\", \"frames\": %d, \"seconds\": %.6f, \"segments\": %llu, "
-                    "\"pixel_samples\": %llu}\n",
+                    "\"pixel_samples\": %llu, \"pixel_format_after\": %lld}\n",
                     backend.c_str(), frames, secs, (unsigned long long)st.segments,
-                    (unsigned long long)st.pixelSamples);
+                    (unsigned long long)st.pixelSamples, hipptGetOption(HIPPT_OPT_PIXEL_FORMAT));
         return 0;
     }
     if (!tracer.initialize(width, height)) {

@@ -1,5 +1,6 @@
 """Invariants of the host SAH BVH builder (replaces BVHNode, RayTracer.h:393-429) and
 result-equivalence of BVH traversal with brute force (the oracle's private BVH)."""
+import os
 import numpy as np
 import pytest
 
@@ -232,3 +233,29 @@ def test_bvh4_quantized_boxes_contain_float_boxes(name):
         ext = f[n, :, 1, used].max(axis=0).astype(np.float64) - f[n, :, 0, used].min(axis=0).astype(np.float64)
         assert np.all(253 * scale[n] >= ext)
         assert np.all((ext == 0) | (253 * scale[n] / 4 < ext))
+
+
+@pytest.mark.parametrize("big", [3.0e38, 3.4e38, -3.4e38])
+def test_quantizer_terminates_near_float_max(big):
+    """Boxes near +-FLT_MAX (the quantizer's scale search had no upper bound and spun
+    forever once the grid origin overflowed): the build returns, the float trees are built, and
+    the scene simply has no 8-bit tree (hipptBvh4QNodeCount 0) when no finite grid covers it.
+    Runs in a subprocess under a timeout so that a regression fails instead of hanging."""
+    import subprocess
+    import sys
+    import textwrap
+    code = textwrap.dedent(f"""
+        import numpy as np, hippt
+        v = np.array([[0, 0, 0, 1, 0, 0, 0, 1, 0], [{big}, 0, 0, {big}, 1, 0, {big}, 0, 1],
+                      [5, 5, 5, 6, 5, 5, 5, 6, 5]], np.float32)
+        b = hippt.Bvh(v)
+        assert sorted(b.order.tolist()) == [0, 1, 2]
+        assert b.nodes4.shape[0] >= 1
+        print(b.nodes4q.shape[0])
+    """)
+    env = dict(os.environ, PYTHONPATH=os.pathsep.join(sys.path))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=60, env=env)
+    assert out.returncode == 0, out.stderr[-2000:]
+    nq = int(out.stdout.strip().splitlines()[-1])
+    # -3.4e38 - pad overflows to -inf: no 8-bit tree; the others still quantize (one node)
+    assert nq == (0 if big < 0 else 1)

@@ -67,6 +67,7 @@ def test_cpp_host_vulkan_and_gl_interfaces_match_oracle(tmp_path, backend, extra
     info = _run("--backend", backend, "--width", 64, "--height", 40, "--spp", 5, "--depth", depth, "--out", out,
                 *extra)
     assert info["backend"] == backend and info["frames"] == 5
+    assert info["pixel_format_after"] == 0  # HIPPT_PIXEL_ARGB restored for other callers
     px = np.fromfile(out, np.uint32).reshape(40, 64)
     _, acc = po.sphere4(64, 40, 0, 5, clamped)
     assert np.array_equal(px, po.rgba8(acc))

@@ -550,6 +550,28 @@ def test_deferred_combine_across_async_calls(pt, name):
     assert np.array_equal(pt.hostPixels(), ora6[0])
 
 
+@pytest.mark.parametrize("call", ["async", "legacy_abi"])
+def test_mesh_to_sphere_switch_flushes_deferred_combine(pt, call):
+    """An async mesh batch leaves its combine pending (Ctx::deferred); a switch to the built-in
+    4-sphere scene followed by a render from frame 0 must run that combine before the legacy
+    kernel overwrites the accumulation, so the image equals a fresh sphere render (the
+    sphere branch did not flush and blended mesh radiance into the sphere image)."""
+    w, h = 40, 23
+    ora = po.sphere4(w, h, 0, 2, 8)
+    pt.uploadMesh(scenes.cornell34())
+    assert pt.initialize(w, h)
+    assert pt.renderFramesAsync(3, 8), pt.lastError()
+    pt.useBuiltinScene(hippt.SCENE_SPHERE4)
+    lib = hippt.load_library()
+    for f in range(2):
+        if call == "async":
+            assert lib.hipptRenderFramesAsync(f, 1, 8, None)
+        else:
+            assert lib.cudaPathTracerRender(f, 8, None, None)
+    got = pt.readback()
+    _assert_same(got[0], got[1], ora[0], ora[1])
+
+
 def test_mesh_row_range_and_two_contexts(pt):
     sc = scenes.cornell34()
     pt.uploadMesh(sc)
@@ -691,6 +713,35 @@ def test_quantized_tree_far_from_origin(pt, offset):
     pt.uploadMesh(sc)
     w, h = 48, 32
     ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
+    pt.setOption(hippt.OPT_LDS_SCENE, 0)
+    for width, quant in ((4, 1), (4, 0), (2, -1)):
+        pt.setOption(hippt.OPT_BVH_WIDTH, width)
+        pt.setOption(hippt.OPT_BVH_QUANT, quant)
+        assert pt.initialize(w, h)
+        assert pt.renderFrames(3, 8)
+        got = pt.readback()
+        _assert_same(got[0], got[1], ora[0], ora[1])
+
+
+def test_quantized_tree_tiny_far_nodes(pt):
+    """tiny nodes far from the ray origin on the 8-bit path.  A cluster of 400
+    triangles of size ~1e-3 (nodes whose extent is ~1e-6 of their distance from the camera) in
+    front of a large backdrop, so that the scene's largest coordinate (and with it the global box
+    pad M * 2^-16) is set by the backdrop: the decoded 8-bit planes stay outside the float planes
+    and no grazing hit is culled (bit-exact against the oracle, 8-bit, float and 2-wide trees)."""
+    rng = np.random.default_rng(11)
+    n = 400
+    centre = np.array([1.0, 2.0, -1500.0]) + rng.normal(scale=0.02, size=(n, 1, 3))
+    tiny = (centre + 1e-3 * rng.normal(size=(n, 3, 3))).reshape(n, 9)
+    back = np.array([[-3000, -3000, -3000, 3000, -3000, -3000, 0, 3000, -3000]], np.float64)
+    verts = np.concatenate([tiny, back]).astype(np.float32)
+    sc = scenes.Scene("tiny_far", verts, (np.arange(n + 1) % 2).astype(np.int32),
+                      np.array([[0.8, 0.7, 0.6], [0.3, 0.5, 0.9]], np.float32),
+                      lookfrom=(1.0, 2.0, 0.0), lookat=(1.0, 2.0, -1500.0), vfov=0.003)
+    pt.uploadMesh(sc)
+    w, h = 48, 32
+    ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
+    assert 0 < np.count_nonzero(ora[0] != ora[0][0, 0])  # the cluster is in the picture
     pt.setOption(hippt.OPT_LDS_SCENE, 0)
     for width, quant in ((4, 1), (4, 0), (2, -1)):
         pt.setOption(hippt.OPT_BVH_WIDTH, width)
