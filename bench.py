@@ -1,15 +1,20 @@
 #!/usr/bin/env python3
 """bench.py — Msamples/s (rays x bounces per second) of the HIP path-tracing megakernel.
 
-Workload (BASELINE.json configs[1]): Cornell-34 scene, 1920x1080, 64 spp, 8 bounces.
+Workload (BASELINE.json configs[1], the default): Cornell-34 scene, 1920x1080, 64 spp, 8 bounces.
 One step = the whole workload once: 64 frames of every pixel (running-average accumulation,
-frames 0..63) through libhippt's C ABI.  With N GPUs (torchrun, one process per GPU) rank r
-renders rows r, r+N, r+2N, ... (interleaved: contiguous bands differ in cost by up to 1.6x) and
-the image is bit-identical for any N.  --scaling weak (default): the step renders 64*N frames
-of the 1080p image (frames 0..64N-1, a progressive render whose sample count grows with the
-GPUs), so every rank traces as many samples as one GPU does alone; --scaling strong: 64
-frames at every N (each rank a 1/N share of a fixed job).  No collective touches the data
-path — ranks only meet at the barriers and the max-over-ranks of the timed interval (gloo, CPU).
+frames 0..63) through libhippt's C ABI.  --preset configN selects another BASELINE workload
+(config2 = the default, config3 blob70k 1080p, config4 blob70k 3840x2160 256 spp — the 8-GPU
+row-tiled job —, config5 the blob70k wavefront A/B).
+
+With N GPUs (torchrun, one process per GPU) rank r renders rows r, r+N, r+2N, ... (interleaved:
+contiguous bands differ in cost by up to 1.6x) and the image is bit-identical for any N.
+--scaling strong (default): the SAME job at every N (each rank a 1/N share of the image's rows;
+the north star's "tile scaling" of a fixed image); --scaling weak: the step renders spp*N frames
+(every rank traces as many samples as one GPU does alone).  No collective touches the data path —
+ranks only meet at the barriers, the max-over-ranks of the timed interval and the untimed
+bookkeeping after it (gloo, CPU).  For N > 1 the line carries `ranks`: each rank's kernel time
+and wall time per step and the max/mean kernel-time imbalance.
 
 value = segments traced by all ranks in the K timed steps / max-over-ranks wall time, in
 millions per second; the segment count is the exact count the kernel accumulates (one per
@@ -28,7 +33,10 @@ Also reported on rank 0:
                 LDS/L2/MALL, not HBM).
   cpu_baseline  the reference CPU path tracer (RayTracer.h + Qt-free RenderWorker, built as
                 oracle/_ref/ref_harness) timed on this box's host cores over a bounded row
-                sample of the same workload.
+                sample of the same workload: the median of 3 runs, with the host's CPU facts
+                (nproc, the affinity mask's size, lscpu's model name, OMP_NUM_THREADS).  If the
+                harness is missing the object says so (value null, an error string) instead of
+                timing a different program; --cpu-baseline port times the FP32 oracle port.
 """
 from __future__ import annotations
 
@@ -53,6 +61,24 @@ BYTES_NODE4 = 112  # 4-wide node: 4 child boxes + 4 child codes
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector (= FP32 MFMA) peak
 FLOP_NODE, FLOP_TRI, FLOP_SHADE = 40, 55, 100  # SURVEY.md §8(d) secondary figure
 
+# BASELINE.json configs[k] as bench workloads (configs[0] is the CPU-only plumbing case)
+PRESETS = {
+    "config2": dict(scene="cornell34", width=1920, height=1080, spp=64, depth=8, path_mode="megakernel"),
+    "config3": dict(scene="blob70k", width=1920, height=1080, spp=64, depth=8, path_mode="megakernel"),
+    "config4": dict(scene="blob70k", width=3840, height=2160, spp=256, depth=8, path_mode="megakernel"),
+    "config5": dict(scene="blob70k", width=1920, height=1080, spp=64, depth=8, path_mode="wavefront"),
+}
+
+
+def baseline_config_index(args) -> int | None:
+    """k of the BASELINE.json configs[k] this run's workload is (None: none of them)."""
+    w = dict(scene=args.scene, width=args.width, height=args.height, spp=args.spp, depth=args.depth,
+             path_mode=args.path_mode)
+    for name, p in PRESETS.items():
+        if p == w:
+            return int(name[-1]) - 1
+    return None
+
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
@@ -68,8 +94,11 @@ def parse():
     p.add_argument("--path-mode", default="megakernel", choices=["megakernel", "wavefront"],
                    help="BASELINE configs[4] A/B: persistent megakernel or wavefront kernels")
     p.add_argument("--wavefront-slots", type=int, default=None)
-    p.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                   help="N GPUs render N*spp frames (weak: fixed work per GPU) or spp frames (strong)")
+    p.add_argument("--preset", default=None, choices=sorted(PRESETS),
+                   help="a BASELINE.json workload (overrides --scene/--width/--height/--spp/--depth/--path-mode)")
+    p.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                   help="N GPUs render spp frames of the image (strong: a fixed job, the default) or "
+                        "N*spp frames (weak: fixed work per GPU)")
     p.add_argument("--split", default="interleave", choices=["interleave", "bands"],
                    help="rows per rank for N>1: interleaved (rank r: rows r, r+N, ...) or contiguous bands")
     p.add_argument("--width", type=int, default=1920)
@@ -82,30 +111,69 @@ def parse():
     p.add_argument("--bvh-width", type=int, default=None, choices=[0, 2, 4],
                    help="megakernel BVH width (HIPPT_OPT_BVH_WIDTH; default automatic)")
     p.add_argument("--cpu-baseline", default="auto", choices=["auto", "reference", "port", "off"])
-    p.add_argument("--cpu-seconds", type=float, default=12.0, help="target CPU sample duration")
+    p.add_argument("--cpu-seconds", type=float, default=8.0, help="target duration of one CPU sample run")
+    p.add_argument("--cpu-runs", type=int, default=3, help="CPU sample runs (the median is reported)")
     p.add_argument("--cpu-threads", type=int, default=None)
     p.add_argument("--pmc", default=None, help="PMC summary JSON for roofline.traffic")
-    return p.parse_args()
+    a = p.parse_args()
+    if a.preset:
+        for k, v in PRESETS[a.preset].items():
+            setattr(a, k, v)
+    return a
 
 
-def cpu_threads(args) -> int:
+def host_cpu_facts() -> dict:
+    """What the CPU baseline ran on: nproc (os.cpu_count, the whole machine), the affinity mask's
+    size, OMP_NUM_THREADS (the GPU box sets it to the box's CPU share, 16 per GPU) and lscpu's
+    model name (read from /proc/cpuinfo, as lscpu does)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return {"nproc": os.cpu_count(), "affinity": affinity, "omp_num_threads": omp or None, "model": model}
+
+
+def cpu_threads(args, facts) -> tuple[int, str]:
+    """Threads for the CPU baseline and the rule that chose them: --cpu-threads, else the
+    affinity mask's size, capped by OMP_NUM_THREADS when set (on the GPU box the mask and nproc
+    cover the whole machine while the box's CPU share is OMP_NUM_THREADS = 16 per GPU)."""
     if args.cpu_threads:
-        return args.cpu_threads
-    n = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    return max(1, min(n if n > 0 else (os.cpu_count() or 1), 16))
+        return args.cpu_threads, "--cpu-threads"
+    if facts["omp_num_threads"] and facts["omp_num_threads"] < facts["affinity"]:
+        return facts["omp_num_threads"], "OMP_NUM_THREADS (the host's CPU share; below the affinity mask)"
+    return facts["affinity"], "affinity mask"
 
 
 def cpu_baseline(args, scene) -> dict | None:
-    """Reference CPU tracer on a bounded sample of rows of the same workload."""
+    """Reference CPU tracer on a bounded sample of rows of the same workload: the median of
+    --cpu-runs runs."""
     if args.cpu_baseline == "off":
         return None
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import pyoracle  # checker / baseline only
     from hippt import scenes as sc_mod
-    threads = cpu_threads(args)
+    facts = host_cpu_facts()
+    threads, rule = cpu_threads(args, facts)
     kind = args.cpu_baseline
     if kind == "auto":
-        kind = "reference" if os.path.exists(pyoracle.REF_HARNESS) else "port"
+        if not os.path.exists(pyoracle.REF_HARNESS):
+            # never a silent substitute: the reference build is missing, say so
+            log("cpu_baseline: oracle/_ref/ref_harness is missing (make -C oracle ref, needs /root/reference)")
+            return {"value": None, "unit": "Msamples/s", "cores": threads, "kind": "reference",
+                    "error": "oracle/_ref/ref_harness missing: the reference CPU tracer was not built "
+                             "(make -C oracle ref in the development container); not timed", "host": facts}
+        kind = "reference"
+    runs = max(1, args.cpu_runs)
     if kind == "reference":
         with tempfile.TemporaryDirectory() as tmp:
             path = os.path.join(tmp, "scene.bin")
@@ -122,24 +190,32 @@ def cpu_baseline(args, scene) -> dict | None:
             per_line = probe["seconds"] / max(1, probe["rows"])
             lines = max(1, min(args.height, int(args.cpu_seconds / max(per_line, 1e-6))))
             stride = max(1, -(-args.height // lines))
-            r = run(stride)
+            rs = sorted((run(stride) for _ in range(runs)), key=lambda r: r["msamples_per_s"])
+        r = rs[len(rs) // 2]
         return {"value": round(r["msamples_per_s"], 4), "unit": "Msamples/s", "cores": threads,
                 "kind": "reference",
                 "sample": f"every {stride}th line ({r['rows']} lines) of {args.width}x{args.height}, {args.spp} spp, "
                           f"depth {args.depth}, "
                           f"{scene.name}; RayTracer.h ray_color + RenderWorker tile pool (tile {r['tile']}), "
-                          f"{r['segments']} segments in {r['seconds']:.2f} s",
+                          f"{r['segments']} segments in {r['seconds']:.2f} s; median of {runs} runs",
+                "runs": [round(x["msamples_per_s"], 4) for x in rs],
+                "threads_rule": rule, "host": facts,
                 "mpixel_samples_per_s": round(r["mpixel_samples_per_s"], 4)}
     ms = pyoracle.MeshScene(scene, args.width, args.height, accel=1)
     t0 = time.perf_counter()
     _, _, segs, ps = ms.frames(0, args.spp, args.depth, y0=0, y1=2, nthreads=threads)
     rate = segs / max(time.perf_counter() - t0, 1e-6)
     rows = max(1, min(args.height, int(args.cpu_seconds * rate / max(segs / 2, 1))))
-    t0 = time.perf_counter()
-    _, _, segs, ps = ms.frames(0, args.spp, args.depth, y0=0, y1=rows, nthreads=threads)
-    dt = time.perf_counter() - t0
-    return {"value": round(segs / dt / 1e6, 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
-            "sample": f"rows 0..{rows - 1}, {args.spp} spp, depth {args.depth}, {scene.name}; FP32 oracle port"}
+    vals = []
+    for _ in range(runs):
+        t0 = time.perf_counter()
+        _, _, segs, ps = ms.frames(0, args.spp, args.depth, y0=0, y1=rows, nthreads=threads)
+        vals.append(segs / (time.perf_counter() - t0) / 1e6)
+    vals.sort()
+    return {"value": round(vals[len(vals) // 2], 4), "unit": "Msamples/s", "cores": threads, "kind": "port",
+            "sample": f"rows 0..{rows - 1}, {args.spp} spp, depth {args.depth}, {scene.name}; FP32 oracle port; "
+                      f"median of {runs} runs",
+            "runs": [round(v, 4) for v in vals], "threads_rule": rule, "host": facts}
 
 
 def load_pmc(args, workload: str):
@@ -297,6 +373,8 @@ def main():
     elapsed = time.perf_counter() - t0
 
     st = pt.stats()
+    # per-rank kernel and wall time per step (untimed bookkeeping: the load balance of the split)
+    per_rank = hd.gather_floats((st["traceMs"] / args.steps, elapsed * 1e3 / args.steps), dist)
     elapsed_max = hd.max_over_ranks(elapsed, dist)
     segments = hd.sum_over_ranks(st["segments"], dist)
     samples = hd.sum_over_ranks(st["pixelSamples"], dist)
@@ -328,6 +406,11 @@ def main():
     roofline = make_roofline(args, pmc, traffic, mean_launch_ms, launches, alg_bytes_launch, flops_launch,
                              counted, achieved)
 
+    k = baseline_config_index(args)
+    workload_label = workload
+    if k is not None:
+        workload_label += (f" (BASELINE configs[{k}])" if world == 1 or args.scaling == "strong"
+                           else f" (BASELINE configs[{k}] per GPU)")
     if rank == 0:
         cpu = cpu_baseline(args, scene) if world == 1 else None
         import zlib
@@ -345,10 +428,7 @@ def main():
             "dtype": "f32",
             "data": "synthetic",
             "config": {
-                "workload": workload + (" (BASELINE configs[1])" if world == 1 or args.scaling == "strong"
-                                        else " (BASELINE configs[1] per GPU)")
-                if args.scene == "cornell34" and args.width == 1920 and args.height == 1080 and args.spp == 64
-                and args.depth == 8 else workload,
+                "workload": workload_label,
                 "scene": args.scene, "triangles": scene.num_tris, "spheres": scene.num_spheres,
                 "path_mode": args.path_mode, "width": args.width, "height": args.height,
                 "spp": frames, "spp_per_gpu_share": args.spp, "max_depth": args.depth,
@@ -366,6 +446,13 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu,
         }
+        if world > 1:
+            kms = [r[0] for r in per_rank]
+            line["ranks"] = {"trace_ms_per_step": [round(x, 4) for x in kms],
+                             "wall_ms_per_step": [round(r[1], 4) for r in per_rank],
+                             "imbalance_max_over_mean": round(max(kms) / max(sum(kms) / len(kms), 1e-9), 4),
+                             "note": "each rank's kernel time (HIP events) and wall time per step; "
+                                     "imbalance = slowest rank's kernel time / the mean"}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.barrier()

@@ -93,3 +93,16 @@ def gather_interleaved(rows: np.ndarray, height: int, dist=None) -> np.ndarray:
         idx = interleaved_rows(r, world, height)
         full[idx] = outs[r].numpy()[: len(idx)]
     return full.view(rows.dtype).reshape((height,) + width_shape)
+
+
+def gather_floats(values, dist=None) -> list:
+    """Every rank's tuple of floats (e.g. its kernel ms and wall time per step), on every rank:
+    [rank 0's values, rank 1's, ...].  Bench bookkeeping only, after the timed region."""
+    vals = [float(v) for v in values]
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return [vals]
+    import torch
+    t = torch.tensor(vals, dtype=torch.float64)
+    outs = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+    dist.all_gather(outs, t)
+    return [o.tolist() for o in outs]

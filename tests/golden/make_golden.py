@@ -15,6 +15,13 @@ them changes the bytes but not the statistics the tests check):
   random_scene  ref_random_scene.scene: one random_scene() (RayTracer.h:599-643) as the
                 reference generated it (its RNG is nondeterministic, so this target only
                 runs when the file is missing or --force is given)
+  headline      oracle_headline_<scene>_<W>x<H>_<spp>.json: the FP32 oracle's (oracle/pt_oracle.c)
+                WHOLE image at the BASELINE headline workloads, configs[1] (cornell34) and
+                configs[2] (blob70k), 1920x1080, 64 spp, 8 bounces: CRC32 of the ARGB words, per-row
+                CRC32s, SHA-256 of the accumulation floats, segment and pixel-sample counts
+                (running-average recurrence of CudaPathTracerKernel.cu:157-178 over frames 0..63).
+                Not the reference binary (CUDA is unbuildable here): the oracle pinned by the
+                other targets.  Minutes of CPU (all cores); not part of the default targets.
 Fixtures are data only: inputs and the reference's outputs.
 """
 from __future__ import annotations
@@ -76,13 +83,44 @@ def make_converge(tmp, only=None) -> None:
         print(name, "mean radiance", img[..., :3].mean(axis=(0, 1)))
 
 
+# (scene, W, H, spp, depth) of BASELINE.json configs[1] and configs[2]
+HEADLINE = [("cornell34", 1920, 1080, 64, 8), ("blob70k", 1920, 1080, 64, 8)]
+
+
+def headline_path(name, w, h, spp):
+    return os.path.join(HERE, f"oracle_headline_{name}_{w}x{h}_{spp}.json")
+
+
+def make_headline(only=None) -> None:
+    import hashlib
+    import time
+    import zlib
+    for name, w, h, spp, depth in HEADLINE:
+        if only and name not in only:
+            continue
+        t0 = time.time()
+        ms = pyoracle.MeshScene(scenes.get_scene(name), w, h, accel=1)
+        px, acc, segs, samples = ms.frames(0, spp, depth, nthreads=os.cpu_count() or 1)
+        d = {"scene": name, "width": w, "height": h, "spp": spp, "max_depth": depth,
+             "generator": "oracle/pt_oracle.c po_mesh_frames (FP32 restatement), tests/golden/make_golden.py headline",
+             "image_crc32": zlib.crc32(px.tobytes()) & 0xFFFFFFFF,
+             "accum_sha256": hashlib.sha256(acc.tobytes()).hexdigest(),
+             "segments": segs, "pixel_samples": samples,
+             "row_crc32": [zlib.crc32(px[y].tobytes()) & 0xFFFFFFFF for y in range(h)]}
+        with open(headline_path(name, w, h, spp), "w") as f:
+            json.dump(d, f)
+        print(name, "crc32", d["image_crc32"], "segments", segs, f"{time.time() - t0:.0f} s")
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("targets", nargs="*", default=["functions", "random_scene", "converge"])
     ap.add_argument("--scenes", nargs="*", help="converge only these scenes")
     ap.add_argument("--force", action="store_true", help="regenerate ref_random_scene.scene")
     a = ap.parse_args()
-    if not os.path.exists(pyoracle.REF_HARNESS_STRICT):
+    if "headline" in a.targets:
+        make_headline(a.scenes)
+    if set(a.targets) - {"headline"} and not os.path.exists(pyoracle.REF_HARNESS_STRICT):
         raise SystemExit("oracle/_ref not built: make -C oracle ref (needs /root/reference)")
     tmp = tempfile.mkdtemp()
     if "functions" in a.targets:

@@ -1,0 +1,70 @@
+"""bench.py's host logic on CPU (no GPU): BASELINE presets and their workload labels, the CPU
+baseline's thread rule and host facts, and that a missing reference harness is reported as
+missing (value null + error) instead of silently timing another program."""
+import importlib.util
+import os
+import sys
+import types
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def _args(bench, argv):
+    old = sys.argv
+    sys.argv = ["bench.py", *argv]
+    try:
+        return bench.parse()
+    finally:
+        sys.argv = old
+
+
+def test_default_is_configs1_strong(bench):
+    a = _args(bench, [])
+    assert (a.scene, a.width, a.height, a.spp, a.depth, a.path_mode) == ("cornell34", 1920, 1080, 64, 8,
+                                                                          "megakernel")
+    assert a.scaling == "strong" and bench.baseline_config_index(a) == 1
+
+
+@pytest.mark.parametrize("preset,k,scene,w,h,spp,mode", [
+    ("config2", 1, "cornell34", 1920, 1080, 64, "megakernel"),
+    ("config3", 2, "blob70k", 1920, 1080, 64, "megakernel"),
+    ("config4", 3, "blob70k", 3840, 2160, 256, "megakernel"),
+    ("config5", 4, "blob70k", 1920, 1080, 64, "wavefront"),
+])
+def test_presets_name_their_baseline_config(bench, preset, k, scene, w, h, spp, mode):
+    a = _args(bench, ["--preset", preset, "--width", "7"])  # a preset overrides the size flags
+    assert (a.scene, a.width, a.height, a.spp, a.depth, a.path_mode) == (scene, w, h, spp, 8, mode)
+    assert bench.baseline_config_index(a) == k
+    a.spp = 32
+    assert bench.baseline_config_index(a) is None
+
+
+def test_cpu_thread_rule(bench):
+    a = _args(bench, [])
+    facts = {"nproc": 256, "affinity": 256, "omp_num_threads": 16, "model": "x"}
+    assert bench.cpu_threads(a, facts)[0] == 16  # the GPU box: the CPU share, not the whole machine
+    facts = {"nproc": 8, "affinity": 8, "omp_num_threads": None, "model": "x"}
+    assert bench.cpu_threads(a, facts) == (8, "affinity mask")
+    a.cpu_threads = 3
+    assert bench.cpu_threads(a, facts) == (3, "--cpu-threads")
+    f = bench.host_cpu_facts()
+    assert f["nproc"] >= 1 and f["affinity"] >= 1
+
+
+def test_missing_reference_harness_is_reported_not_substituted(bench, monkeypatch, tmp_path):
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    monkeypatch.setattr(pyoracle, "REF_HARNESS", str(tmp_path / "no_such_harness"))
+    a = _args(bench, [])
+    cb = bench.cpu_baseline(a, types.SimpleNamespace(name="cornell34"))
+    assert cb["value"] is None and cb["kind"] == "reference" and "missing" in cb["error"]

@@ -44,6 +44,9 @@ def _worker(rank, world, port, out_dir, split="bands"):
             full_acc = hd.gather_interleaved(acc, H, dist)
         total_segs = hd.sum_over_ranks(segs, dist)
         slowest = hd.max_over_ranks(float(rank + 1), dist)
+        # bench.py's per-rank bookkeeping (kernel ms, wall ms per step) on every rank
+        per_rank = hd.gather_floats((rank + 0.5, 2.0 * rank), dist)
+        assert per_rank == [[r + 0.5, 2.0 * r] for r in range(world)]
         if rank == 0:
             np.save(os.path.join(out_dir, "px.npy"), full_px)
             np.save(os.path.join(out_dir, "acc.npy"), full_acc)
@@ -88,3 +91,4 @@ def test_gather_without_process_group_is_identity():
     a = np.arange(12, dtype=np.uint32).reshape(3, 4)
     assert hd.gather_bands(a, 3) is a
     assert hd.max_over_ranks(2.5) == 2.5 and hd.sum_over_ranks(7) == 7
+    assert hd.gather_floats((1, 2.5)) == [[1.0, 2.5]]

@@ -1,0 +1,99 @@
+"""The BASELINE.json workloads at their real sizes (GPU), through the C ABI.
+
+* configs[1] (Cornell-34) and configs[2] (blob70k), 1920x1080, 64 spp, 8 bounces: the WHOLE image
+  the bench times equals the oracle's whole image (golden CRC32 of the ARGB words, SHA-256 of the
+  accumulation floats, exact segment and sample counts; tests/golden/make_golden.py headline,
+  oracle/pt_oracle.c over frames 0..63 with the running average of CudaPathTracerKernel.cu:157-178).
+* configs[3] (blob70k, 3840x2160, 8 GPUs row-tiled) rehearsed on one GPU: 8 contexts on device 0
+  (hipptSetDevices([0]*8), interleaved rows) and 8 one-process-per-GPU shares
+  (hipptSetRowInterleave(r, 8), gathered on the host) each give the one-context image bit for bit,
+  and sampled rows equal the oracle.  2 spp keeps the oracle's rows to seconds.
+"""
+import json
+import os
+import zlib
+
+import numpy as np
+import pytest
+
+import hippt
+import pyoracle as po
+from hippt import scenes
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+@pytest.fixture()
+def pt():
+    t = hippt.PathTracer()
+    t.setDevices([])
+    t.setRowRange(0, 0)
+    t.setOption(hippt.OPT_DEVICE_ROWS, 1)
+    t.resetStats()
+    yield t
+    t.setDevices([])
+    t.setRowRange(0, 0)
+    hippt.load_library().cudaPathTracerShutdown()
+
+
+@pytest.mark.parametrize("name", ["cornell34", "blob70k"])
+def test_headline_image_equals_oracle_golden(pt, name):
+    import hashlib
+    with open(os.path.join(GOLDEN, f"oracle_headline_{name}_1920x1080_64.json")) as f:
+        g = json.load(f)
+    pt.uploadMesh(scenes.get_scene(name))
+    assert pt.initialize(g["width"], g["height"]), pt.lastError()
+    pt.resetStats()
+    # the bench's call: one batch of all 64 frames, async, then the readback's sync
+    assert pt.renderFramesAsync(g["spp"], g["max_depth"]), pt.lastError()
+    px, acc = pt.readback()
+    st = pt.stats()
+    rows = [y for y in range(g["height"]) if zlib.crc32(px[y].tobytes()) & 0xFFFFFFFF != g["row_crc32"][y]]
+    assert not rows, f"{len(rows)} rows differ from the oracle, first {rows[:8]}"
+    assert zlib.crc32(px.tobytes()) & 0xFFFFFFFF == g["image_crc32"]
+    assert hashlib.sha256(acc.tobytes()).hexdigest() == g["accum_sha256"]
+    assert st["segments"] == g["segments"] and st["pixelSamples"] == g["pixel_samples"]
+
+
+def test_config4_row_split_on_one_gpu(pt):
+    w, h, spp, depth, n = 3840, 2160, 2, 8, 8
+    sc = scenes.blob70k()
+    pt.uploadMesh(sc)
+    assert pt.initialize(w, h), pt.lastError()
+    assert pt.renderFrames(spp, depth), pt.lastError()
+    one = pt.readback()
+    one_segs = pt.stats()["segments"]
+    # 8 contexts on one device, interleaved rows (the in-process multi-GPU split)
+    pt.setDevices([0] * n)
+    pt.setOption(hippt.OPT_DEVICE_ROWS, 1)
+    assert pt.initialize(w, h), pt.lastError()
+    pt.resetStats()
+    assert pt.renderFrames(spp, depth), pt.lastError()
+    st = pt.stats()
+    assert st["numDevices"] == n and st["segments"] == one_segs
+    eight = pt.readback()
+    assert np.array_equal(eight[0], one[0]) and eight[1].tobytes() == one[1].tobytes()
+    assert np.array_equal(pt.hostPixels(), one[0])
+    # 8 one-process-per-GPU shares (bench.py --gpus 8: rank r renders rows r, r+8, ...), gathered
+    pt.setDevices([])
+    px = np.zeros((h, w), np.uint32)
+    acc = np.zeros((h, w, 4), np.float32)
+    segs = 0
+    for r in range(n):
+        pt.setRowInterleave(r, n)
+        assert pt.initialize(w, h), pt.lastError()
+        pt.resetStats()
+        assert pt.renderFrames(spp, depth), pt.lastError()
+        segs += pt.stats()["segments"]
+        got = pt.readback()
+        px[r::n], acc[r::n] = got[0][r::n], got[1][r::n]
+    assert segs == one_segs
+    assert np.array_equal(px, one[0]) and acc.tobytes() == one[1].tobytes()
+    # and the image is the oracle's on sampled rows (top, middle through the mesh, bottom)
+    ms = po.MeshScene(sc, w, h, accel=1)
+    for y0 in (0, h // 2 - 1, h - 2):
+        ora = ms.frames(0, spp, depth, y0=y0, y1=y0 + 2)
+        assert np.array_equal(one[0][y0:y0 + 2], ora[0])
+        assert one[1][y0:y0 + 2].tobytes() == ora[1].tobytes()
