@@ -702,4 +702,35 @@ bool quantize_bvh4(const Bvh4 &in, std::vector<uint32_t> &out) {
     return true;
 }
 
+bool hybrid_bvh4(const Bvh4 &b, const std::vector<uint32_t> &q, int topNodes, std::vector<uint32_t> &out) {
+    const size_t n = b.nodes.size() / kNode4Words;
+    out.clear();
+    if (q.size() != n * kNode4QWords || topNodes < 1 || size_t(topNodes) > n) return false;
+    const size_t top = size_t(topNodes);
+    auto code = [&](int32_t c) -> uint32_t {
+        if (c < 0) return uint32_t(c);  // leaf
+        const size_t k = size_t(c);
+        return uint32_t(k < top ? k * 128 : top * 128 + (k - top) * 64);
+    };
+    out.resize(top * kNode4Words + (n - top) * kNode4QWords);
+    for (size_t k = 0; k < top; ++k) {
+        uint32_t *d = &out[k * kNode4Words];
+        std::memcpy(d, &b.nodes[k * kNode4Words], kNode4Words * sizeof(uint32_t));
+        for (int i = 0; i < 4; ++i) d[24 + i] = code(int32_t(d[24 + i]));
+    }
+    for (size_t k = top; k < n; ++k) {
+        uint32_t *d = &out[top * kNode4Words + (k - top) * kNode4QWords];
+        std::memcpy(d, &q[k * kNode4QWords], kNode4QWords * sizeof(uint32_t));
+        for (int i = 0; i < 4; ++i) {
+            const int32_t c = int32_t(d[12 + i]);
+            if (c >= 0 && size_t(c) < top) {  // never for a breadth-first top; kept total
+                out.clear();
+                return false;
+            }
+            d[12 + i] = code(c);
+        }
+    }
+    return true;
+}
+
 }  // namespace hippt

@@ -92,4 +92,14 @@ int order_bvh4_top(Bvh4 &b, int topNodes);
 constexpr int kNode4QWords = 16;
 bool quantize_bvh4(const Bvh4 &in, std::vector<uint32_t> &out);
 
+// Hybrid device layout of a 4-wide tree (the megakernel over trees in global memory, with the top
+// of the tree in LDS): nodes 0..topNodes-1 (the breadth-first top, order_bvh4_top) as 128-byte
+// float nodes (Bvh4 words) at byte k*128, every other node k as its 64-byte 8-bit node (the
+// quantize_bvh4 words `q` of the same tree) at byte topNodes*128 + (k - topNodes)*64.  Interior
+// child codes become those BYTE offsets (a code below topNodes*128 is a float node), leaf codes
+// stay.  The top's children may be 8-bit nodes; a bottom node's children are always bottom nodes
+// (the breadth-first prefix holds every ancestor of its nodes).  `b` and `q` carry node-index
+// codes.  Returns false if q is empty (no 8-bit tree) or topNodes is out of range.
+bool hybrid_bvh4(const Bvh4 &b, const std::vector<uint32_t> &q, int topNodes, std::vector<uint32_t> &out);
+
 }  // namespace hippt

@@ -79,6 +79,8 @@ struct Ctx {
     float4 *nodes = nullptr, *tris = nullptr, *shade = nullptr, *mats = nullptr;
     float4 *nodes4 = nullptr;  // 4-wide BVH (same primitive order as nodes)
     float4 *nodes4q = nullptr; // the 4-wide BVH with 8-bit child boxes
+    float4 *nodes4h = nullptr; // hybrid layout (float top + 8-bit nodes) for hybridTop top nodes
+    int hybridTop = -1;
     int *spill = nullptr;      // 4-wide traversal: per-lane stack spill area
     size_t spillBytes = 0;
     // wavefront path-state pool (allocated on first use)
@@ -106,6 +108,10 @@ struct SceneHost {
     int numTris = 0, numNodes = 0, levels = 0;  // numTris: primitive records (triangles + spheres)
     std::vector<float4> nodes4;                 // 4-wide BVH (bvh_builder.h Bvh4)
     std::vector<float4> nodes4q;                // quantize_bvh4 of it
+    hippt::Bvh4 bvh4;                           // the 4-wide tree with node-index codes ...
+    std::vector<uint32_t> q4;                   // ... and its 8-bit nodes (hybrid_bvh4 inputs)
+    std::vector<float4> hybrid;                 // hybrid_bvh4 for hybridTop top nodes (built on use)
+    int hybridTop = -1;
     int numNodes4 = 0, levels4 = 0, stackBound4 = 0;
     bool full = false;                          // spheres or non-Lambertian materials
     double lookfrom[3] = {0, 0, 0}, lookat[3] = {0, 0, -1}, vup[3] = {0, 1, 0};
@@ -246,7 +252,9 @@ void free_scene_buffers(Ctx &c) {
     (void)hipFree(c.mats);
     (void)hipFree(c.nodes4);
     (void)hipFree(c.nodes4q);
-    c.nodes = c.tris = c.shade = c.mats = c.nodes4 = c.nodes4q = nullptr;
+    (void)hipFree(c.nodes4h);
+    c.nodes = c.tris = c.shade = c.mats = c.nodes4 = c.nodes4q = c.nodes4h = nullptr;
+    c.hybridTop = -1;
     c.sceneVersion = -1;
 }
 
@@ -357,6 +365,30 @@ bool ensure_scene(Ctx &c, const char **err) {
         !up(c.mats, s.scene.mats) || !up(c.nodes4, s.scene.nodes4) || !up(c.nodes4q, s.scene.nodes4q))
         return false;
     c.sceneVersion = s.scene.version;
+    return true;
+}
+
+// The hybrid node layout (bvh_builder.h hybrid_bvh4) for `top` top-of-tree nodes: built on the
+// host once per (scene, top) and uploaded to the context's device.
+bool ensure_hybrid(Ctx &c, int top, const char **err) {
+    State &s = S();
+    SceneHost &sc = s.scene;
+    if (sc.hybridTop != top) {
+        std::vector<uint32_t> w;
+        if (!hippt::hybrid_bvh4(sc.bvh4, sc.q4, top, w)) return fail(err, "hybrid BVH layout failed");
+        sc.hybrid.assign(w.size() / 4, float4{});
+        std::memcpy(sc.hybrid.data(), w.data(), w.size() * sizeof(uint32_t));
+        sc.hybridTop = top;
+    }
+    if (c.hybridTop == top && c.nodes4h) return true;
+    HIP_TRY(hipSetDevice(c.device));
+    HIP_TRY(hipStreamSynchronize(c.stream));
+    (void)hipFree(c.nodes4h);
+    c.nodes4h = nullptr;
+    c.hybridTop = -1;
+    HIP_TRY(hipMalloc(&c.nodes4h, sc.hybrid.size() * sizeof(float4)));
+    HIP_TRY(hipMemcpy(c.nodes4h, sc.hybrid.data(), sc.hybrid.size() * sizeof(float4), hipMemcpyHostToDevice));
+    c.hybridTop = top;
     return true;
 }
 
@@ -695,8 +727,13 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 // only: the megakernel reads the top of the tree (62-70% of the visits) from LDS,
                 // where the float nodes need no decode (blob70k 19.0 G 8-bit, 20.4 G float, r2v).
                 // (scenes with boxes near +-FLT_MAX have no 8-bit tree: quantize_bvh4 failed)
-                const bool quant = wide && !ldsScene && !s.scene.nodes4q.empty() &&
-                                   (s.bvhQuant == 1 || (s.bvhQuant == -1 && !s.scene.full && s.pathMode == 1));
+                // Hybrid (HIPPT_OPT_BVH_QUANT 2, megakernel): the top of the tree as float nodes in LDS
+                // (no decode where most visits are) and 8-bit nodes below it (4 loads instead of 7
+                // where the texture addresser binds); falls back to 8-bit nodes without a top.
+                bool hybrid = wide && !ldsScene && !s.scene.nodes4q.empty() && s.pathMode == 0 && s.bvhQuant == 2 &&
+                              s.ldsTopNodes != 0;
+                bool quant = wide && !ldsScene && !s.scene.nodes4q.empty() &&
+                             (s.bvhQuant >= 1 || (s.bvhQuant == -1 && !s.scene.full && s.pathMode == 1));
                 // The top of a global-memory tree in LDS (megakernel and wavefront extend): the
                 // breadth-first prefix of the node array that the LDS budget of the resident blocks
                 // leaves beside the stack (automatic), or HIPPT_OPT_LDS_TOP_NODES nodes.  The
@@ -706,12 +743,13 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 // Pinhole cameras at a nonzero origin start every ray at cam.origin exactly
                 // (origin + 0*offset), so their pool entries carry no origin.
                 const bool pool = s.pathMode == 0 && wide && !quant && (s.cameraPool == 1 || (s.cameraPool == -1 && ldsScene));
+                if (hybrid) quant = false;  // (pool: off, as for 8-bit nodes)
                 const bool pinhole = cam.lens_radius == 0.0f && cam.origin[0] != 0.0f && cam.origin[1] != 0.0f &&
                                      cam.origin[2] != 0.0f;
                 const int poolWords = pool ? (pinhole ? hippt::kPoolWordsPinhole : hippt::kPoolWordsFull) : 0;
                 unsigned topBytes = 0;
                 if (topTree && s.ldsTopNodes != 0) {
-                    const size_t nodeBytes = quant ? 64 : 128;
+                    const size_t nodeBytes = quant ? 64 : 128;  // hybrid: a float top
                     size_t n = size_t(std::min(numNodes, kTopOrderNodes));
                     if (s.ldsTopNodes > 0) {
                         n = std::min(n, size_t(s.ldsTopNodes));
@@ -722,15 +760,22 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                     }
                     topBytes = unsigned(n * nodeBytes);
                 }
+                if (hybrid && topBytes == 0) {  // no LDS left for a top: plain 8-bit nodes
+                    hybrid = false;
+                    quant = true;
+                }
+                const int fmt = !wide ? hippt::kWide2 : hybrid ? hippt::kWideHybrid : quant ? hippt::kWideQuant
+                                                                                      : hippt::kWideFloat;
+                if (hybrid && !ensure_hybrid(c, int(topBytes / 128), err)) return false;
                 const long long occKey =
                     occupancy_key(s.scene.version, stackDepth, ldsScene, s.scene.full, wide, quant, spills) ^
-                    ((long long)topBytes << 40) ^ ((long long)poolWords << 36);
+                    ((long long)topBytes << 40) ^ ((long long)poolWords << 36) ^ ((long long)hybrid << 35);
                 if (c.occKey != occKey) {
                     const int ln = ldsScene ? numNodes : 0, lt = ldsScene ? numTris : 0, lm = ldsScene ? numMats : 0;
-                    c.meshBlocksPerCu[0] = hippt::mesh_blocks_per_cu(false, s.scene.full, wide, quant, stackDepth,
-                                                                     ln, lt, spills, topBytes, lm, poolWords);
-                    c.meshBlocksPerCu[1] = hippt::mesh_blocks_per_cu(true, s.scene.full, wide, quant, stackDepth,
-                                                                     ln, lt, spills, topBytes, lm, poolWords);
+                    c.meshBlocksPerCu[0] = hippt::mesh_blocks_per_cu(false, s.scene.full, fmt, stackDepth, ln, lt,
+                                                                     spills, topBytes, lm, poolWords);
+                    c.meshBlocksPerCu[1] = hippt::mesh_blocks_per_cu(true, s.scene.full, fmt, stackDepth, ln, lt,
+                                                                     spills, topBytes, lm, poolWords);
                     c.occKey = occKey;
                 }
                 s.activeTopBytes = topBytes;
@@ -749,7 +794,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         HIP_TRY(hipMemsetAsync(scratch, 0, size_t(total) * 3 * sizeof(float), c.stream));
                     } else {
                         hippt::MeshParams p{};
-                        p.nodes = quant ? c.nodes4q : wide ? c.nodes4 : c.nodes;
+                        p.nodes = hybrid ? c.nodes4h : quant ? c.nodes4q : wide ? c.nodes4 : c.nodes;
                         p.tris = c.tris;
                         p.shade = c.shade;
                         p.mats = c.mats;
@@ -790,7 +835,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         // leaves the leaf loop once <= 48 lanes hold a leaf (Cornell 28.4 -> 31.3 G).
                         p.leafExit = unsigned(s.leafExit >= 0 ? s.leafExit : ldsScene ? 4 : 17);
                         p.nodeExit = unsigned(s.nodeExit >= 0 ? s.nodeExit : 48);
-                        p.wide = quant ? 2 : wide ? 1 : 0;
+                        p.wide = fmt;
                         p.stackCap = stackCap;
                         p.topBytes = topBytes;
                         p.rngTable = nullptr;
@@ -993,6 +1038,10 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
     (void)hippt::quantize_bvh4(bvh4, q);  // empty on failure: the float nodes serve every path
     sc.nodes4q.assign(q.size() / 4, float4{});
     std::memcpy(sc.nodes4q.data(), q.data(), q.size() * sizeof(uint32_t));
+    sc.bvh4 = bvh4;
+    sc.q4 = q;
+    sc.hybrid.clear();
+    sc.hybridTop = -1;
     if (bvh4.nodes.size() / hippt::kNode4Words >= (1u << 24)) return fail(err, "4-wide BVH too large (2^24 nodes)");
     // device layouts of the 4-wide trees: an interior child's code is its node's BYTE offset (the
     // kernels address a node without a multiply; leaf codes and the root, 0, are unchanged)
@@ -1382,7 +1431,7 @@ extern "C" bool hipptSetOption(int key, long long value) {
         s.stackCap = int(value);
         return true;
     case HIPPT_OPT_BVH_QUANT:
-        if (value < -1 || value > 1) return false;
+        if (value < -1 || value > 2) return false;
         s.bvhQuant = int(value);
         return true;
     case HIPPT_OPT_LDS_TOP_NODES:

@@ -67,9 +67,11 @@ struct MeshParams {
     unsigned chunk;        // items per queue grab (multiple of 64)
     unsigned leafExit;     // node loop exits once <= leafExit lanes still search for a leaf
     unsigned nodeExit;     // leaf loop exits once <= nodeExit lanes still hold a leaf (0: never)
-    // 4-wide BVH: wide = 1 (Bvh4 layout, 8 float4 per node) or 2 (quantize_bvh4 layout, 4 float4
-    // per node; global-memory scenes only); LDS stack content capacity and the per-lane spill
-    // area (spillCap entries per lane of the persistent grid; null if never used)
+    // Node format (kWide*): 0 the 2-wide tree; 1 the 4-wide tree (Bvh4 layout, 8 float4 per node);
+    // 2 quantize_bvh4 layout (4 float4 per node; global-memory scenes only); 3 hybrid_bvh4 (the
+    // top's topBytes as float nodes, read from LDS, then 8-bit nodes; global-memory scenes only).
+    // LDS stack content capacity and the per-lane spill area (spillCap entries per lane of the
+    // persistent grid; null if never used)
     int wide;
     int stackCap;
     int spillCap;
@@ -93,6 +95,9 @@ struct MeshParams {
 };
 
 
+// MeshParams::wide
+enum { kWide2 = 0, kWideFloat = 1, kWideQuant = 2, kWideHybrid = 3 };
+
 // Material kinds (RayTracer.h:473-540) and the sphere flag of a shading record.
 enum { kLambertian = 0, kMetal = 1, kDielectric = 2 };
 constexpr int kShadeSphere = 1 << 30;
@@ -115,8 +120,8 @@ hipError_t launch_combine(const CombineParams &p, hipStream_t s);
 constexpr size_t kRngTableBytes = size_t(4) << 32;
 hipError_t launch_rng_table(uint32_t *table, hipStream_t s);
 // Resident mesh-kernel blocks per CU for a given LDS stack depth and LDS scene size.
-int mesh_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,
-                       int ldsTris, bool spill, unsigned topBytes = 0, int ldsMats = 0, int poolWords = 0);
+int mesh_blocks_per_cu(bool countTraversal, bool full, int fmt, int stackDepth, int ldsNodes, int ldsTris, bool spill,
+                       unsigned topBytes = 0, int ldsMats = 0, int poolWords = 0);
 size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide, unsigned topBytes = 0, int ldsMats = 0,
                       int poolWords = 0);
 // camera-ray pool words per ray: item, rng, direction (+ origin unless every ray starts at the

@@ -265,7 +265,8 @@ __device__ __forceinline__ void pool_take(const MeshParams &P, const float *pool
     }
 }
 
-template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE, bool QUANT, bool SPILL = true, bool POOL = false>
+template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE, bool QUANT, bool SPILL = true, bool POOL = false,
+          bool HYBRID = false>
 __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_EU : HIPPT_MESH_WAVES_PER_EU) HIPPT_SGPR_ATTR void mesh_kernel(MeshParams P) {
     static_assert(!QUANT || (WIDE && !LDS_SCENE), "quantized nodes: 4-wide global-memory traversal only");
 #ifdef HIPPT_DEBUG_TIMELINE
@@ -438,7 +439,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         if (!CAP || __any(busy(T))) do {
             prof<STATS>(pc, 2);
             if (WIDE)
-                traverse_round_wide<nodeF4, STATS, FULL, QUANT, SPILL, LDS_SCENE, TOP>(
+                traverse_round_wide<nodeF4, STATS, FULL, QUANT, SPILL, LDS_SCENE, TOP, HYBRID>(
                     T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit, S, P.topBytes);
             else
                 traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
@@ -600,43 +601,48 @@ static constexpr int kMaxResidentBlocks = 800 / (HIPPT_NUM_SGPR + 16) < 8 ? 800 
 size_t mesh_lds_block_budget() { return (size_t(160u << 10) / kMaxResidentBlocks) & ~size_t(511); }
 
 using MeshFn = void (*)(MeshParams);
-// node formats: 2-wide, 4-wide float, 4-wide quantized (global memory only)
+// node formats (MeshParams::wide): 2-wide, 4-wide float, 4-wide quantized, 4-wide hybrid (float
+// top in LDS, quantized below it); the quantized formats are for global-memory trees only
 // 4-wide trees whose stack bound fits the LDS capacity run a variant without the spill/refill
 // code (timed builds; the counting builds keep one variant, the results are the same)
 // (the camera-ray pool: 4-wide float-node kernels)
 template <bool STATS, bool FULL, bool SPILL, bool POOL>
-static MeshFn mesh_fn_wide(bool lds, bool quant) {
+static MeshFn mesh_fn_wide(bool lds, int fmt) {
     if (lds) return mesh_kernel<STATS, true, FULL, true, false, SPILL, POOL>;
-    return quant ? mesh_kernel<STATS, false, FULL, true, true, SPILL>
-                 : mesh_kernel<STATS, false, FULL, true, false, SPILL, POOL>;
+    if (fmt == kWideHybrid) return mesh_kernel<STATS, false, FULL, true, true, SPILL, false, true>;
+    return fmt == kWideQuant ? mesh_kernel<STATS, false, FULL, true, true, SPILL>
+                             : mesh_kernel<STATS, false, FULL, true, false, SPILL, POOL>;
 }
 template <bool STATS, bool FULL>
-static MeshFn mesh_fn_fmt(bool lds, bool wide, bool quant, bool spill, bool pool) {
-    if (!wide) return lds ? mesh_kernel<STATS, true, FULL, false, false> : mesh_kernel<STATS, false, FULL, false, false>;
+static MeshFn mesh_fn_fmt(bool lds, int fmt, bool spill, bool pool) {
+    if (fmt == kWide2) return lds ? mesh_kernel<STATS, true, FULL, false, false> : mesh_kernel<STATS, false, FULL, false, false>;
     if (STATS || spill)
-        return pool ? mesh_fn_wide<STATS, FULL, true, true>(lds, quant) : mesh_fn_wide<STATS, FULL, true, false>(lds, quant);
-    return pool ? mesh_fn_wide<STATS, FULL, false, true>(lds, quant) : mesh_fn_wide<STATS, FULL, false, false>(lds, quant);
+        return pool ? mesh_fn_wide<STATS, FULL, true, true>(lds, fmt) : mesh_fn_wide<STATS, FULL, true, false>(lds, fmt);
+    return pool ? mesh_fn_wide<STATS, FULL, false, true>(lds, fmt) : mesh_fn_wide<STATS, FULL, false, false>(lds, fmt);
 }
-static MeshFn mesh_fn(bool count, bool lds, bool full, bool wide, bool quant, bool spill, bool pool) {
+static MeshFn mesh_fn(bool count, bool lds, bool full, int fmt, bool spill, bool pool) {
     if (count)
-        return full ? mesh_fn_fmt<true, true>(lds, wide, quant, spill, pool)
-                    : mesh_fn_fmt<true, false>(lds, wide, quant, spill, pool);
-    return full ? mesh_fn_fmt<false, true>(lds, wide, quant, spill, pool)
-                : mesh_fn_fmt<false, false>(lds, wide, quant, spill, pool);
+        return full ? mesh_fn_fmt<true, true>(lds, fmt, spill, pool) : mesh_fn_fmt<true, false>(lds, fmt, spill, pool);
+    return full ? mesh_fn_fmt<false, true>(lds, fmt, spill, pool) : mesh_fn_fmt<false, false>(lds, fmt, spill, pool);
 }
 
 hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hipStream_t s) {
     if (p.stackDepth < 1 || p.stackDepth > kStackDepth) return hipErrorInvalidValue;
     if (p.wide && (p.stackCap < 1 || p.stackCap + 2 > p.stackDepth)) return hipErrorInvalidValue;
     const bool lds = p.ldsScene != 0;
-    if (p.topBytes && (lds || !p.wide || p.topBytes % (p.wide == 2 ? 64u : 128u) || p.topBytes > (unsigned(p.numNodes) << (p.wide == 2 ? 6 : 7))))
+    if (p.wide < kWide2 || p.wide > kWideHybrid || (lds && p.wide >= kWideQuant)) return hipErrorInvalidValue;
+    // the top of the tree: whole nodes of the LDS-read format (8-bit nodes only for kWideQuant)
+    if (p.topBytes && (lds || p.wide == kWide2 || p.topBytes % (p.wide == kWideQuant ? 64u : 128u) ||
+                       p.topBytes > (unsigned(p.numNodes) << (p.wide == kWideQuant ? 6 : 7))))
         return hipErrorInvalidValue;
+    if (p.wide == kWideHybrid && !p.topBytes) return hipErrorInvalidValue;  // hybrid trees start in LDS
     const bool pool = p.poolWords != 0;
-    if (pool && (p.wide != 1 || (p.poolWords != kPoolWordsPinhole && p.poolWords != kPoolWordsFull))) return hipErrorInvalidValue;
+    if (pool && (p.wide != kWideFloat || (p.poolWords != kPoolWordsPinhole && p.poolWords != kPoolWordsFull)))
+        return hipErrorInvalidValue;
     const size_t bytes = mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0, p.wide != 0, p.topBytes,
                                         lds ? p.numMats : 0, p.poolWords);
     if (pool && p.poolOffset != bytes - size_t(p.poolWords) * kMeshBlock * sizeof(float)) return hipErrorInvalidValue;
-    const MeshFn fn = mesh_fn(countTraversal, lds, p.full != 0, p.wide != 0, p.wide == 2 && !lds, p.spill != nullptr, pool);
+    const MeshFn fn = mesh_fn(countTraversal, lds, p.full != 0, p.wide, p.spill != nullptr, pool);
     if (p.wide && (lds || p.topBytes || pool)) {
         const hipError_t e = check_lds_at_zero(reinterpret_cast<const void *>(fn));
         if (e != hipSuccess) return e;
@@ -653,13 +659,14 @@ hipError_t launch_combine(const CombineParams &p, hipStream_t s) {
     return hipGetLastError();
 }
 
-int mesh_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,
-                       int ldsTris, bool spill, unsigned topBytes, int ldsMats, int poolWords) {
+int mesh_blocks_per_cu(bool countTraversal, bool full, int fmt, int stackDepth, int ldsNodes, int ldsTris, bool spill,
+                       unsigned topBytes, int ldsMats, int poolWords) {
     int n = 0;
     const bool lds = ldsNodes > 0;
-    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, wide, topBytes, ldsMats, poolWords);
+    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, fmt != kWide2, topBytes, ldsMats, poolWords);
     hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &n, mesh_fn(countTraversal, lds, full, wide, quant && wide && !lds, spill, poolWords != 0), kMeshBlock, bytes);
+        &n, mesh_fn(countTraversal, lds, full, lds && fmt >= kWideQuant ? kWideFloat : fmt, spill, poolWords != 0),
+        kMeshBlock, bytes);
     if (e != hipSuccess || n <= 0) n = 1;
     // the query ignores the trap handler's SGPRs (kMaxResidentBlocks): a larger persistent grid
     // leaves blocks waiting for a slot until others finish

@@ -782,13 +782,17 @@ __device__ __forceinline__ void cas(unsigned &ka, int &ca, unsigned &kb, int &cb
 // breadth-first) also sit at LDS address 0; a visit to one of them reads LDS, which spares the
 // texture addresser (TA) — the unit that bounds the traversal of global-memory trees — the loads
 // every ray makes at the top of the tree.
+// HYBRID (with QUANT and TOP; bvh_builder.h hybrid_bvh4): the top is 128-byte float nodes (read
+// from LDS, no decode) and every node below it a 64-byte 8-bit node in global memory (4 loads
+// instead of 7 where the TA binds); a node byte offset below topBytes is a top node.
 template <int NODE_F4, bool STATS, bool FULL, bool QUANT = false, bool SPILL = true, bool LDS0 = false,
-          bool TOP = false>
+          bool TOP = false, bool HYBRID = false>
 __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *my, const float4 *nodes,
                                                     const float4 *tris, unsigned long long &nvis,
                                                     unsigned long long &ntest, unsigned *pc, unsigned leafExit,
                                                     unsigned nodeExit, const SpillArea &S,
                                                     unsigned topBytes = 0) {
+    static_assert(!HYBRID || (QUANT && TOP), "hybrid trees: 8-bit nodes below an LDS top");
     const float tmin = 0.001f;
     // near-row byte offsets of this ray's octant within a node (x at 0/16, y at 32/48, z at 64/80)
     const unsigned sx = near_row(r.ix), sy = near_row(r.iy) | 32u, sz = near_row(r.iz) | 64u;
@@ -800,13 +804,14 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
         const unsigned nb = unsigned(T.cur);  // interior codes are node byte offsets
         unsigned k0, k1, k2, k3;
         int4 ch;
-        if (!QUANT) {
+        const bool topVisit = TOP && nb < topBytes;
+        if (!QUANT || (HYBRID && topVisit)) {
             // 128-byte float nodes (LDS and global): nb's low 7 bits are zero, so the octant's
             // near row is nb | s and the far row its ^ 16
             const unsigned ax = nb | sx, ay = nb | sy, az = nb | sz;
             // LDS0: the nodes are the LDS scene copy at LDS address 0
             float4 nx, fx, ny, fy, nz, fz, cw;
-            if (LDS0 || (TOP && nb < topBytes)) {
+            if (LDS0 || HYBRID || topVisit) {
                 nx = lds_ld4(ax);
                 fx = lds_ld4(ax ^ 16u);
                 ny = lds_ld4(ay);
@@ -839,7 +844,7 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
             // 64-byte node (bvh_builder.h quantize_bvh4): 4 loads instead of 7.  Plane q of axis
             // a enters the slab test as t = q*(s*inv) + (o*inv - o_ray*inv).
             float4 o, qf, q2, cw;
-            if (TOP && nb < topBytes) {
+            if (!HYBRID && topVisit) {
                 o = lds_ld4(nb);
                 qf = lds_ld4(nb + 16u);
                 q2 = lds_ld4(nb + 32u);

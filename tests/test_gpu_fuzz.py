@@ -1,7 +1,7 @@
 """Seeded random scenes (GPU): triangle soups with degenerate, tiny, huge, axis-aligned and
 edge-sharing triangles, overlapping spheres, all three materials, pinhole and thin-lens cameras,
-rendered through the C ABI in the LDS-resident, global-memory (float and 8-bit nodes), 2-wide and
-wavefront paths, and
+rendered through the C ABI in the LDS-resident, global-memory (float, 8-bit and hybrid nodes),
+2-wide and wavefront paths, and
 compared bit for bit (ARGB words, accumulation floats, segment counts) with the oracle.
 
 The named benchmark scenes exercise the hot path at scale; these exercise the geometry the
@@ -78,6 +78,7 @@ MODES = {
     "global": ((hippt.OPT_LDS_SCENE, 0), (hippt.OPT_BVH_WIDTH, 0), (hippt.OPT_PATH_MODE, 0)),
     "wide2": ((hippt.OPT_LDS_SCENE, 0), (hippt.OPT_BVH_WIDTH, 2), (hippt.OPT_PATH_MODE, 0)),
     "quant8": ((hippt.OPT_LDS_SCENE, 0), (hippt.OPT_BVH_WIDTH, 0), (hippt.OPT_BVH_QUANT, 1)),
+    "hybrid": ((hippt.OPT_LDS_SCENE, 0), (hippt.OPT_BVH_WIDTH, 0), (hippt.OPT_BVH_QUANT, 2)),
     "wavefront": ((hippt.OPT_LDS_SCENE, 1), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_PATH_MODE, 1),
                   (hippt.OPT_WAVEFRONT_SLOTS, 500)),
 }

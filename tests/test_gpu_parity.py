@@ -324,15 +324,17 @@ def test_bvh_width_and_stack_spill_do_not_change_results(pt, name):
 def test_lds_top_of_tree_does_not_change_results(pt, name):
     """Trees read from global memory with the top of the tree copied into LDS
     (HIPPT_OPT_LDS_TOP_NODES: none, the root alone, 5 and 85 nodes, the automatic size, which
-    covers all of cornell34's 16 nodes), float and 8-bit nodes, the spilling LDS stack (cap 4)
-    and the default: the oracle's image bit for bit.  Counting builds report LDS-served visits
-    exactly when a top is in LDS."""
+    covers all of cornell34's 16 nodes), float, 8-bit and hybrid nodes (float top, 8-bit below;
+    with no top it falls back to 8-bit nodes), the spilling LDS stack (cap 4) and the default:
+    the oracle's image bit for bit.  Counting builds report LDS-served visits exactly when a top
+    is in LDS."""
     sc = scenes.get_scene(name)
     pt.uploadMesh(sc)
     pt.setOption(hippt.OPT_LDS_SCENE, 0)
     w, h = (40, 24) if name == "random_scene" else (56, 40)
     ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
-    quants = (0,) if name == "random_scene" else (0, 1)
+    # 0 float nodes, 1 8-bit nodes (top too), 2 hybrid: float top in LDS, 8-bit nodes below
+    quants = (0, 2) if name == "random_scene" else (0, 1, 2)
     for quant in quants:
         for cap in (0, 4):
             for top in (0, 1, 5, 85, -1):
@@ -460,14 +462,14 @@ def test_small_stack_cap_on_deep_lds_scene(pt, mode):
 
 def test_quantized_tree_grid_aligned_geometry(pt):
     """Integer-coordinate cubes (every child-box plane on its node's power-of-two grid) read
-    from global memory with 8-bit child boxes: bit-exact against the oracle, as the float
-    4-wide and the 2-wide trees."""
+    from global memory with 8-bit child boxes (whole tree, and below a float LDS top): bit-exact
+    against the oracle, as the float 4-wide and the 2-wide trees."""
     sc = scenes.voxel_scene(6)
     pt.uploadMesh(sc)
     pt.setOption(hippt.OPT_LDS_SCENE, 0)
     w, h = 64, 48
     ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
-    for width, quant in ((4, 1), (4, 0), (2, -1)):
+    for width, quant in ((4, 1), (4, 2), (4, 0), (2, -1)):
         pt.setOption(hippt.OPT_BVH_WIDTH, width)
         pt.setOption(hippt.OPT_BVH_QUANT, quant)
         assert pt.initialize(w, h)
@@ -714,7 +716,7 @@ def test_quantized_tree_far_from_origin(pt, offset):
     w, h = 48, 32
     ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
     pt.setOption(hippt.OPT_LDS_SCENE, 0)
-    for width, quant in ((4, 1), (4, 0), (2, -1)):
+    for width, quant in ((4, 1), (4, 2), (4, 0), (2, -1)):
         pt.setOption(hippt.OPT_BVH_WIDTH, width)
         pt.setOption(hippt.OPT_BVH_QUANT, quant)
         assert pt.initialize(w, h)
@@ -743,7 +745,7 @@ def test_quantized_tree_tiny_far_nodes(pt):
     ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
     assert 0 < np.count_nonzero(ora[0] != ora[0][0, 0])  # the cluster is in the picture
     pt.setOption(hippt.OPT_LDS_SCENE, 0)
-    for width, quant in ((4, 1), (4, 0), (2, -1)):
+    for width, quant in ((4, 1), (4, 2), (4, 0), (2, -1)):
         pt.setOption(hippt.OPT_BVH_WIDTH, width)
         pt.setOption(hippt.OPT_BVH_QUANT, quant)
         assert pt.initialize(w, h)
