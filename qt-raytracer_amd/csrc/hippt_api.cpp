@@ -368,6 +368,20 @@ bool ensure_scene(Ctx &c, const char **err) {
     return true;
 }
 
+// Low bits of a packed child key (trace::child_key_p) that give an LDS-resident 4-wide tree's child
+// codes back when sign-extended: interior codes are node byte offsets < numNodes*128, leaf codes
+// ~(first<<4 | count) with first + count <= numPrims; one more bit for the sign.  At most 16 for a
+// scene that fits the LDS copy (24 KB: < 192 nodes, < 384 primitives), which leaves the entry
+// distance 7 or more mantissa bits (Cornell-34: 12 bits, 11 mantissa bits) to order children by.
+unsigned packed_ref_bits(int numNodes, int numPrims) {
+    const unsigned long long maxMag =
+        std::max<unsigned long long>((unsigned long long)std::max(numNodes, 1) * 128ull,
+                                     ((unsigned long long)numPrims << 4) + 16ull);
+    unsigned bits = 1;
+    while ((1ull << (bits - 1)) < maxMag) ++bits;  // magnitude < 2^(bits-1)
+    return std::max(bits, 8u);
+}
+
 // The hybrid node layout (bvh_builder.h hybrid_bvh4) for `top` top-of-tree nodes: built on the
 // host once per (scene, top) and uploaded to the context's device.
 bool ensure_hybrid(Ctx &c, int top, const char **err) {
@@ -838,6 +852,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.wide = fmt;
                         p.stackCap = stackCap;
                         p.topBytes = topBytes;
+                        p.refBits = ldsScene && wide ? packed_ref_bits(numNodes, numTris) : 0u;
                         p.rngTable = nullptr;
                         p.poolWords = poolWords;
                         p.poolOffset = unsigned(hippt::mesh_lds_bytes(stackDepth, ldsScene ? numNodes : 0,

@@ -79,6 +79,9 @@ struct MeshParams {
     // 4-wide trees in global memory: bytes of the node array's prefix (the top of the tree,
     // breadth-first, bvh_builder.h order_bvh4_top) copied to LDS address 0 and read from there
     unsigned topBytes;
+    // LDS-resident 4-wide trees: low bits of a packed child key that carry the child's code
+    // (trace::child_key_p; hippt_api.cpp packed_ref_bits)
+    unsigned refBits;
     // random_in_unit_sphere memoized (null: the rejection loop): entry 2^32-word table, see
     // launch_rng_table
     const uint32_t *rngTable;

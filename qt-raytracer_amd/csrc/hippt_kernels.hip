@@ -200,6 +200,12 @@ __device__ unsigned long long g_timeline[65536 * 6];
 #define HIPPT_REJECT_CAP 0
 #endif
 
+// LDS-resident 4-wide trees sort packed child keys (trace::child_key_p: codes in the keys' low
+// bits, the sorting network as unsigned min/max pairs); 0: keys and codes sorted as pairs
+#ifndef HIPPT_PACKED_KEYS
+#define HIPPT_PACKED_KEYS 1
+#endif
+
 #ifndef HIPPT_WIDE_WAVES_PER_EU
 #define HIPPT_WIDE_WAVES_PER_EU 7
 #endif
@@ -301,7 +307,19 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         for (int i = threadIdx.x; i < P.numMats * 2; i += kMeshBlock) sMats[i] = P.mats[i];
         mats = sMats;
         if (WIDE) {
-            for (int i = threadIdx.x; i < P.numNodes * kLdsNode4F4; i += kMeshBlock) sNodes[i] = P.nodes[i];
+            // packed keys: the copy's code rows hold each code's low refBits bits (child_key_p merges
+            // them into the key with one v_and_or)
+            const unsigned refMask = HIPPT_PACKED_KEYS ? (1u << P.refBits) - 1u : ~0u;
+            for (int i = threadIdx.x; i < P.numNodes * kLdsNode4F4; i += kMeshBlock) {
+                float4 v = P.nodes[i];
+                if (HIPPT_PACKED_KEYS && (i & 7) == 6) {
+                    v.x = __uint_as_float(__float_as_uint(v.x) & refMask);
+                    v.y = __uint_as_float(__float_as_uint(v.y) & refMask);
+                    v.z = __uint_as_float(__float_as_uint(v.z) & refMask);
+                    v.w = __uint_as_float(__float_as_uint(v.w) & refMask);
+                }
+                sNodes[i] = v;
+            }
         } else {
             for (int i = threadIdx.x; i < P.numNodes * 4; i += kMeshBlock)
                 sNodes[(i >> 2) * kLdsNodeF4 + (i & 3)] = P.nodes[i];
@@ -439,8 +457,9 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         if (!CAP || __any(busy(T))) do {
             prof<STATS>(pc, 2);
             if (WIDE)
-                traverse_round_wide<nodeF4, STATS, FULL, QUANT, SPILL, LDS_SCENE, TOP, HYBRID>(
-                    T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit, S, P.topBytes);
+                traverse_round_wide<nodeF4, STATS, FULL, QUANT, SPILL, LDS_SCENE, TOP, HYBRID,
+                                    LDS_SCENE && bool(HIPPT_PACKED_KEYS)>(
+                    T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit, S, P.topBytes, P.refBits);
             else
                 traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
         } while (__popcll(__ballot(busy(T))) > unsigned(P.waveThreshold));
@@ -636,6 +655,7 @@ hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hip
                        p.topBytes > (unsigned(p.numNodes) << (p.wide == kWideQuant ? 6 : 7))))
         return hipErrorInvalidValue;
     if (p.wide == kWideHybrid && !p.topBytes) return hipErrorInvalidValue;  // hybrid trees start in LDS
+    if (lds && p.wide == kWideFloat && (p.refBits < 8 || p.refBits > 20)) return hipErrorInvalidValue;
     const bool pool = p.poolWords != 0;
     if (pool && (p.wide != kWideFloat || (p.poolWords != kPoolWordsPinhole && p.poolWords != kPoolWordsFull)))
         return hipErrorInvalidValue;

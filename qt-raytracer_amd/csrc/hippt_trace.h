@@ -701,12 +701,17 @@ __device__ __forceinline__ void refill_bottom(Trav &T, int *my, const SpillArea 
     T.sp = n * kMeshBlock;
 }
 
-template <bool SPILL = true>
-__device__ __forceinline__ int pop_wide(Trav &T, int *my, const SpillArea &S) {
+// The child code in a packed key's low refBits bits (child_key_p), sign-extended.
+__device__ __forceinline__ int key_code(unsigned key, unsigned refBits) {
+    return __builtin_amdgcn_sbfe(int(key), 0u, refBits);  // v_bfe_i32: sign-extended low bits
+}
+
+template <bool SPILL = true, bool PACKED = false>
+__device__ __forceinline__ int pop_wide(Trav &T, int *my, const SpillArea &S, unsigned refBits = 0) {
     if (SPILL && T.sp == 0 && T.ovf != 0) refill_bottom(T, my, S);
     if (T.sp == 0) return kDone;
     T.sp -= kMeshBlock;
-    return my[T.sp];
+    return PACKED ? key_code(unsigned(my[T.sp]), refBits) : my[T.sp];
 }
 
 // min(a, b) as one v_min_f32: fminf() of the loop-carried bestT makes the compiler quieten a
@@ -775,6 +780,33 @@ __device__ __forceinline__ void cas(unsigned &ka, int &ca, unsigned &kb, int &cb
     cb = sw ? c : cb;
 }
 
+// Packed child keys (PACKED, LDS-resident scenes; child_key_p): the entry distance's bits with the
+// child's code in the low `refBits` bits, (bits & ~mask) | (code & mask); a miss is all ones.  The
+// LDS copy of the nodes holds the codes already masked (mesh_kernel's scene copy).  An interior code (a
+// node byte offset) and a leaf code (~(first<<4 | count)) of a scene that fits the LDS copy are
+// small enough in magnitude that their low refBits bits, sign-extended, give them back
+// (hippt_api.cpp packed_ref_bits): the sorted keys ARE the sorted codes, so the sorting network
+// is 5 unsigned min/max pairs (no compare + 4 selects per exchange moving the codes along), and the
+// stack holds keys.  Truncating the distance to its high bits only reorders near-equal children,
+// and the closest hit is argmin (t, primitive id): no result bit depends on the visiting order.
+template <bool PACKED>
+__device__ __forceinline__ unsigned child_key_p(float nx, float fx, float ny, float fy, float nz, float fz,
+                                                const Ray &r, float tmin, float bestT, int code, unsigned mask) {
+    if (!PACKED) return child_key(nx, fx, ny, fy, nz, fz, r, tmin, bestT);
+    const float ax = fmaf(nx, r.ix, -r.oix), bx = fmaf(fx, r.ix, -r.oix);
+    const float ay = fmaf(ny, r.iy, -r.oiy), by = fmaf(fy, r.iy, -r.oiy);
+    const float az = fmaf(nz, r.iz, -r.oiz), bz = fmaf(fz, r.iz, -r.oiz);
+    const float n = fmaxf(fmaxf(ax, ay), fmaxf(az, tmin));
+    const float f = fminf(fminf(bx, by), fmin_raw(bz, bestT));
+    return n <= f ? (__float_as_uint(n) & ~mask) | unsigned(code) : 0xffffffffu;  // code: pre-masked
+}
+
+__device__ __forceinline__ void cas_key(unsigned &ka, unsigned &kb) {
+    const unsigned lo = min(ka, kb), hi = max(ka, kb);
+    ka = lo;
+    kb = hi;
+}
+
 // traverse_round over the 4-wide tree: a node visit tests its four child boxes, descends into
 // the nearest hit child and pushes the other hit children far to near.  SPILL=false: the tree's
 // stack bound fits the LDS capacity (no spill/refill code in the loop).
@@ -785,14 +817,17 @@ __device__ __forceinline__ void cas(unsigned &ka, int &ca, unsigned &kb, int &cb
 // HYBRID (with QUANT and TOP; bvh_builder.h hybrid_bvh4): the top is 128-byte float nodes (read
 // from LDS, no decode) and every node below it a 64-byte 8-bit node in global memory (4 loads
 // instead of 7 where the TA binds); a node byte offset below topBytes is a top node.
+// PACKED (LDS-resident scenes): packed child keys (pack_key), refBits low bits carrying the code.
 template <int NODE_F4, bool STATS, bool FULL, bool QUANT = false, bool SPILL = true, bool LDS0 = false,
-          bool TOP = false, bool HYBRID = false>
+          bool TOP = false, bool HYBRID = false, bool PACKED = false>
 __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *my, const float4 *nodes,
                                                     const float4 *tris, unsigned long long &nvis,
                                                     unsigned long long &ntest, unsigned *pc, unsigned leafExit,
                                                     unsigned nodeExit, const SpillArea &S,
-                                                    unsigned topBytes = 0) {
+                                                    unsigned topBytes = 0, unsigned refBits = 0) {
     static_assert(!HYBRID || (QUANT && TOP), "hybrid trees: 8-bit nodes below an LDS top");
+    static_assert(!PACKED || (LDS0 && !QUANT), "packed keys: LDS-resident float trees");
+    const unsigned refMask = PACKED ? (1u << refBits) - 1u : 0u;
     const float tmin = 0.001f;
     // near-row byte offsets of this ray's octant within a node (x at 0/16, y at 32/48, z at 64/80)
     const unsigned sx = near_row(r.ix), sy = near_row(r.iy) | 32u, sz = near_row(r.iz) | 64u;
@@ -829,10 +864,10 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
                 cw = ld4(nodes, nb + 96u);
             }
             ch = *reinterpret_cast<const int4 *>(&cw);
-            k0 = child_key(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, r, tmin, T.bestT);
-            k1 = child_key(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, r, tmin, T.bestT);
-            k2 = child_key(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z, r, tmin, T.bestT);
-            k3 = child_key(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w, r, tmin, T.bestT);
+            k0 = child_key_p<PACKED>(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, r, tmin, T.bestT, ch.x, refMask);
+            k1 = child_key_p<PACKED>(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, r, tmin, T.bestT, ch.y, refMask);
+            k2 = child_key_p<PACKED>(nx.z, fx.z, ny.z, fy.z, nz.z, fz.z, r, tmin, T.bestT, ch.z, refMask);
+            k3 = child_key_p<PACKED>(nx.w, fx.w, ny.w, fy.w, nz.w, fz.w, r, tmin, T.bestT, ch.w, refMask);
             if (STATS && (k0 & k1 & k2 & k3) == 0xffffffffu) {
                 const unsigned u = child_key(nx.x, fx.x, ny.x, fy.x, nz.x, fz.x, r, tmin, INFINITY) &
                                    child_key(nx.y, fx.y, ny.y, fy.y, nz.y, fz.y, r, tmin, INFINITY) &
@@ -875,28 +910,45 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
         // hit children: a miss key is all ones (bit 31), a hit key a positive float's bits
         const int nh = 4 - int((k0 >> 31) + (k1 >> 31) + (k2 >> 31) + (k3 >> 31));
         if (STATS) ++pc[kNhHist + nh];
-        // sorting network (0,1)(2,3)(0,2)(1,3)(1,2), codes carried along: c0 nearest
-        int c0 = ch.x, c1 = ch.y, c2 = ch.z, c3 = ch.w;
-        cas(k0, c0, k1, c1);
-        cas(k2, c2, k3, c3);
-        cas(k0, c0, k2, c2);
-        cas(k1, c1, k3, c3);
-        cas(k1, c1, k2, c2);
+        // sorting network (0,1)(2,3)(0,2)(1,3)(1,2), codes carried along (or inside the keys):
+        // c0 nearest
+        int c0, c1, c2, c3;
+        if (PACKED) {
+            cas_key(k0, k1);
+            cas_key(k2, k3);
+            cas_key(k0, k2);
+            cas_key(k1, k3);
+            cas_key(k1, k2);
+            c0 = key_code(k0, refBits);  // the stack holds the keys themselves
+            c1 = int(k1);
+            c2 = int(k2);
+            c3 = int(k3);
+        } else {
+            c0 = ch.x;
+            c1 = ch.y;
+            c2 = ch.z;
+            c3 = ch.w;
+            cas(k0, c0, k1, c1);
+            cas(k2, c2, k3, c3);
+            cas(k0, c0, k2, c2);
+            cas(k1, c1, k3, c3);
+            cas(k1, c1, k2, c2);
+        }
         if (SPILL && T.sp + (nh - 1) * kMeshBlock > S.cap * kMeshBlock) spill_bottom(T, my, S, nh - 1);
         // push c[nh-1] .. c1 (c1 on top); unused writes land in the spare slots above
         my[T.sp] = nh == 4 ? c3 : (nh == 3 ? c2 : c1);
         my[T.sp + kMeshBlock] = nh == 4 ? c2 : c1;
         my[T.sp + 2 * kMeshBlock] = c1;
         T.sp += nh > 1 ? (nh - 1) * kMeshBlock : 0;
-        T.cur = nh > 0 ? c0 : pop_wide<SPILL>(T, my, S);
+        T.cur = nh > 0 ? c0 : pop_wide<SPILL, PACKED>(T, my, S, refBits);
         // postpone the first leaf reached and keep descending
         if (T.cur < 0 && T.cur != kDone && T.leaf == 0) {
             T.leaf = T.cur;
-            T.cur = pop_wide<SPILL>(T, my, S);
+            T.cur = pop_wide<SPILL, PACKED>(T, my, S, refBits);
         }
         if (__popcll(__ballot((T.leaf | T.cur) >= 0)) <= leafExit) break;
     }
-    auto popw = [&] { return pop_wide<SPILL>(T, my, S); };
+    auto popw = [&] { return pop_wide<SPILL, PACKED>(T, my, S, refBits); };
     while (T.leaf != 0) {
         prof<STATS>(pc, 4);
         leaf_step<STATS, FULL, decltype(popw), !LDS0>(T, r, tris, ntest, pc, popw);
