@@ -294,6 +294,9 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     // Trees in global memory (4-wide): the top of the tree (P.topBytes of the node array) at LDS
     // address 0, then the stack.
     constexpr bool TOP = WIDE && !LDS_SCENE;
+    // packed child keys: the Lambertian kernel over LDS-resident 4-wide trees (Cornell +0.8%; the
+    // general kernel lost 4.3% with them, cornell_mixed, round 3 A/B)
+    constexpr bool PACKED = WIDE && LDS_SCENE && !FULL && bool(HIPPT_PACKED_KEYS);
     int *const stk = LDS_SCENE ? lds + P.numNodes * ldsNodeF4 * 4 : lds + (TOP ? (P.topBytes >> 2) : 0u);
     int *const my = stk + threadIdx.x;
 
@@ -309,10 +312,10 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         if (WIDE) {
             // packed keys: the copy's code rows hold each code's low refBits bits (child_key_p merges
             // them into the key with one v_and_or)
-            const unsigned refMask = HIPPT_PACKED_KEYS ? (1u << P.refBits) - 1u : ~0u;
+            const unsigned refMask = PACKED ? (1u << P.refBits) - 1u : ~0u;
             for (int i = threadIdx.x; i < P.numNodes * kLdsNode4F4; i += kMeshBlock) {
                 float4 v = P.nodes[i];
-                if (HIPPT_PACKED_KEYS && (i & 7) == 6) {
+                if (PACKED && (i & 7) == 6) {
                     v.x = __uint_as_float(__float_as_uint(v.x) & refMask);
                     v.y = __uint_as_float(__float_as_uint(v.y) & refMask);
                     v.z = __uint_as_float(__float_as_uint(v.z) & refMask);
@@ -457,8 +460,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         if (!CAP || __any(busy(T))) do {
             prof<STATS>(pc, 2);
             if (WIDE)
-                traverse_round_wide<nodeF4, STATS, FULL, QUANT, SPILL, LDS_SCENE, TOP, HYBRID,
-                                    LDS_SCENE && bool(HIPPT_PACKED_KEYS)>(
+                traverse_round_wide<nodeF4, STATS, FULL, QUANT, SPILL, LDS_SCENE, TOP, HYBRID, PACKED>(
                     T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit, S, P.topBytes, P.refBits);
             else
                 traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
