@@ -220,11 +220,14 @@ def cpu_baseline(args, scene) -> dict | None:
 
 def load_pmc(args, workload: str):
     """HBM bytes per launch from a tools/profile.sh summary of this exact workload: --pmc, else
-    profiles/pmc_summary.json (the default workload), else the newest profiles/<tag>_pmc.json."""
+    profiles/pmc_summary.json (the default workload), else the newest profiles/**/<name>_pmc.json."""
     prof = os.path.join(REPO, "profiles")
+    # this round's summaries first, then the rest (newest round first; the archive last)
     paths = [args.pmc] if args.pmc else (
         [os.path.join(prof, "pmc_summary.json")]
-        + sorted(glob.glob(os.path.join(prof, "*_pmc.json")), reverse=True))
+        + sorted(glob.glob(os.path.join(prof, "round*", "*_pmc.json")), reverse=True)
+        + sorted(glob.glob(os.path.join(prof, "*_pmc.json")), reverse=True)
+        + sorted(glob.glob(os.path.join(prof, "archive", "*_pmc.json")), reverse=True))
     for path in paths:
         try:
             with open(path) as f:

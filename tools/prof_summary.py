@@ -50,8 +50,15 @@ def counters(path, skip):
 
 
 def main():
-    tag = sys.argv[1]
-    root = sys.argv[2] if len(sys.argv) > 2 else os.path.join("gpurun_out", f"prof_{tag}")
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("tag", help="profile.sh tag (reads gpurun_out/prof_TAG unless --root)")
+    ap.add_argument("--root", default=None)
+    ap.add_argument("--out", default="profiles", help="directory (repo-relative) for the summary files")
+    ap.add_argument("--name", default=None, help="file stem of the summaries (default: the tag)")
+    a = ap.parse_args()
+    tag = a.tag
+    root = a.root or os.path.join("gpurun_out", f"prof_{tag}")
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     bench = load_json_line(os.path.join(root, "kt_bench.json"))
     lps = bench["roofline"]["launches_per_step"]
@@ -101,15 +108,20 @@ def main():
         if c.get("TA_BUSY_avr") and c.get("TA_FLAT_READ_WAVEFRONTS_sum") else None,
         "bench_value_msamples_s": bench["value"],
     }
-    prof_dir = os.path.join(repo, "profiles")
+    prof_dir = os.path.join(repo, a.out)
+    name = a.name or tag
     os.makedirs(prof_dir, exist_ok=True)
-    # bench.py reads pmc_summary.json for roofline.traffic of its default workload (Cornell);
-    # any other workload keeps its counters beside its summary
+    # bench.py reads profiles/pmc_summary.json for roofline.traffic of its default workload
+    # (Cornell); every workload also keeps its counters beside its summary (<name>_pmc.json, which
+    # bench.py finds by workload)
     default = workload.startswith("cornell34 1920x1080 64spp depth8") and "wavefront" not in workload
-    with open(os.path.join(prof_dir, "pmc_summary.json" if default else f"{tag}_pmc.json"), "w") as f:
+    if default:
+        with open(os.path.join(repo, "profiles", "pmc_summary.json"), "w") as f:
+            json.dump(summary, f, indent=1)
+    with open(os.path.join(prof_dir, f"{name}_pmc.json"), "w") as f:
         json.dump(summary, f, indent=1)
     stats_csv = open(os.path.join(root, "kt", "run_kernel_stats.csv")).read()
-    with open(os.path.join(prof_dir, f"{tag}_summary.md"), "w") as f:
+    with open(os.path.join(prof_dir, f"{name}_summary.md"), "w") as f:
         f.write(f"# rocprofv3 summary `{tag}` — {workload}\n\n")
         f.write("Command: `bash tools/profile.sh` (bench.py --steps 3 --warmup 1 under rocprofv3 "
                 "--kernel-trace --stats, then separate --pmc passes).\n\n")
