@@ -231,10 +231,6 @@ enum {
                                        batch's launch on the same device (beside its paths) instead of as a
                                        launch of its own, whenever nothing reads the image in between (1), or
                                        never (0); -1 (default): automatic.  Same results either way */
-    , HIPPT_OPT_TRIS40 = 28         /* Lambertian triangle scenes: leaves start at even primitive slots and the
-                                       global-memory traversal reads 40-byte triangle records (a 2-triangle
-                                       leaf in 5 loads instead of 6) (1, default), or 48-byte records only
-                                       (0); next upload.  Same results either way */
 };
 /* Output frame word formats (HIPPT_OPT_PIXEL_FORMAT).  Both map an accumulated colour c to
  * sqrt(clamp(c, 0, 1)) per channel.

@@ -702,43 +702,6 @@ bool quantize_bvh4(const Bvh4 &in, std::vector<uint32_t> &out) {
     return true;
 }
 
-void align_leaves(Bvh &bvh, int align) {
-    if (align <= 1) return;
-    struct Leaf {
-        int first, count;
-    };
-    std::vector<Leaf> leaves;
-    const size_t n = bvh.nodes.size() / kNodeWords;
-    for (size_t k = 0; k < n; ++k)
-        for (int c = 0; c < 2; ++c) {
-            const int32_t code = int32_t(bvh.nodes[k * kNodeWords + 12 + size_t(c)]);
-            if (code >= 0) continue;
-            const int v = ~code;
-            if ((v & 15) != 0) leaves.push_back({v >> 4, v & 15});
-        }
-    std::sort(leaves.begin(), leaves.end(), [](const Leaf &a, const Leaf &b) { return a.first < b.first; });
-    std::vector<int> newFirst(bvh.order.size() + 1, -1);
-    int pos = 0;
-    for (const Leaf &l : leaves) {
-        pos = (pos + align - 1) / align * align;
-        newFirst[size_t(l.first)] = pos;
-        pos += l.count;
-    }
-    pos = (pos + align - 1) / align * align;
-    std::vector<int> order(size_t(pos), -1);
-    for (const Leaf &l : leaves)
-        for (int j = 0; j < l.count; ++j) order[size_t(newFirst[size_t(l.first)] + j)] = bvh.order[size_t(l.first + j)];
-    for (size_t k = 0; k < n; ++k)
-        for (int c = 0; c < 2; ++c) {
-            uint32_t &w = bvh.nodes[k * kNodeWords + 12 + size_t(c)];
-            const int32_t code = int32_t(w);
-            if (code >= 0 || (~code & 15) == 0) continue;
-            const int v = ~code;
-            w = uint32_t(leaf_code(newFirst[size_t(v >> 4)], v & 15));
-        }
-    bvh.order.swap(order);
-}
-
 bool hybrid_bvh4(const Bvh4 &b, const std::vector<uint32_t> &q, int topNodes, std::vector<uint32_t> &out) {
     const size_t n = b.nodes.size() / kNode4Words;
     out.clear();

@@ -59,12 +59,6 @@ bool build_bvh_boxes(const float *boxes, int numPrims, float extentHint, Bvh &ou
 
 inline int32_t leaf_code(int first, int count) { return ~((first << 4) | count); }
 
-// Moves every leaf of a 2-wide tree to an even first index (a multiple of `align`), inserting
-// unreferenced padding slots (order[k] = -1) between leaves; leaf codes and the order are rewritten,
-// the tree shape is unchanged.  Used for the 40-byte triangle records (hippt_device.h
-// MeshParams::tris40), whose pairs must start on 16-byte boundaries.
-void align_leaves(Bvh &bvh, int align);
-
 // 4-wide BVH collapsed from a 2-wide one (same leaves, so the same primitive order): each
 // node opens the interior child of largest surface area until it has 4 children.  128-byte
 // nodes, children in SoA: lo.x[4] hi.x[4] lo.y[4] hi.y[4] lo.z[4] hi.z[4] code[4] pad[4];

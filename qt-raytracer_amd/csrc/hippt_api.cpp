@@ -76,7 +76,7 @@ struct Ctx {
     unsigned *queue = nullptr;
     unsigned long long *stats = nullptr;
     int sceneVersion = -1;
-    float4 *nodes = nullptr, *tris = nullptr, *shade = nullptr, *mats = nullptr, *tris40 = nullptr;
+    float4 *nodes = nullptr, *tris = nullptr, *shade = nullptr, *mats = nullptr;
     float4 *nodes4 = nullptr;  // 4-wide BVH (same primitive order as nodes)
     float4 *nodes4q = nullptr; // the 4-wide BVH with 8-bit child boxes
     float4 *nodes4h = nullptr; // hybrid layout (float top + 8-bit nodes) for hybridTop top nodes
@@ -105,7 +105,6 @@ struct SceneHost {
     int kind = HIPPT_SCENE_SPHERE4;
     int version = 0;
     std::vector<float4> nodes, tris, shade, mats;  // device layouts (hippt_device.h MeshParams)
-    std::vector<float4> tris40;                     // MeshParams::tris40 (Lambertian triangle scenes)
     int numTris = 0, numNodes = 0, levels = 0;  // numTris: primitive records (triangles + spheres)
     std::vector<float4> nodes4;                 // 4-wide BVH (bvh_builder.h Bvh4)
     std::vector<float4> nodes4q;                // quantize_bvh4 of it
@@ -155,7 +154,6 @@ struct State {
     int bvhQuant = -1;  // 4-wide global-memory traversal over 8-bit child boxes (-1: automatic)
     int ldsTopNodes = -1;  // top-of-tree nodes copied into LDS for global-memory trees (-1: automatic)
     bool rngTable = false;  // memoized random_in_unit_sphere (HIPPT_OPT_RNG_TABLE)
-    bool tris40 = true;     // 40-byte triangle records for Lambertian scenes (HIPPT_OPT_TRIS40; next upload)
     int pixelFormat = HIPPT_PIXEL_ARGB;  // output frame words (HIPPT_OPT_PIXEL_FORMAT)
     int cameraPool = -1;  // megakernel camera-ray pool (HIPPT_OPT_CAMERA_POOL; -1: automatic)
     int fuseCombine = -1;  // combine inside the next megakernel launch (HIPPT_OPT_FUSE_COMBINE)
@@ -255,8 +253,7 @@ void free_scene_buffers(Ctx &c) {
     (void)hipFree(c.nodes4);
     (void)hipFree(c.nodes4q);
     (void)hipFree(c.nodes4h);
-    (void)hipFree(c.tris40);
-    c.nodes = c.tris = c.shade = c.mats = c.nodes4 = c.nodes4q = c.nodes4h = c.tris40 = nullptr;
+    c.nodes = c.tris = c.shade = c.mats = c.nodes4 = c.nodes4q = c.nodes4h = nullptr;
     c.hybridTop = -1;
     c.sceneVersion = -1;
 }
@@ -365,8 +362,7 @@ bool ensure_scene(Ctx &c, const char **err) {
         return true;
     };
     if (!up(c.nodes, s.scene.nodes) || !up(c.tris, s.scene.tris) || !up(c.shade, s.scene.shade) ||
-        !up(c.mats, s.scene.mats) || !up(c.nodes4, s.scene.nodes4) || !up(c.nodes4q, s.scene.nodes4q) ||
-        !up(c.tris40, s.scene.tris40))
+        !up(c.mats, s.scene.mats) || !up(c.nodes4, s.scene.nodes4) || !up(c.nodes4q, s.scene.nodes4q))
         return false;
     c.sceneVersion = s.scene.version;
     return true;
@@ -814,7 +810,6 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         hippt::MeshParams p{};
                         p.nodes = hybrid ? c.nodes4h : quant ? c.nodes4q : wide ? c.nodes4 : c.nodes;
                         p.tris = c.tris;
-                        p.tris40 = s.scene.tris40.empty() ? nullptr : c.tris40;
                         p.shade = c.shade;
                         p.mats = c.mats;
                         p.scratch = scratch;
@@ -1029,12 +1024,6 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
     hippt::Bvh bvh;
     std::string msg;
     if (!hippt::build_bvh_boxes(boxes.data(), numPrims, extent, bvh, msg, s.bvh)) return fail(err, msg);
-    // Lambertian triangle scenes also get 40-byte triangle records (MeshParams::tris40: a 2-primitive
-    // leaf in 5 loads instead of 6), whose leaves start at even slots: padding slots between leaves
-    const bool tris40 = !full && s.tris40;
-    if (tris40) hippt::align_leaves(bvh, 2);
-    const int numSlots = int(bvh.order.size());  // primitive slots in leaf order (with padding)
-    if (numSlots >= (1 << 27)) return fail(err, "too many primitives");
     SceneHost &sc = s.scene;
     sc.nodes.assign(bvh.nodes.size() / 4, float4{});
     std::memcpy(sc.nodes.data(), bvh.nodes.data(), bvh.nodes.size() * sizeof(uint32_t));
@@ -1045,7 +1034,7 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
         // (leaves of <= 2 primitives: Cornell +1.6-1.9%, cornell_mixed +1.0%, r3ap/r3aq), the
         // greedy one for trees read from global memory (SAH-optimal: blob70k -9%, random_scene -4%)
         auto fits = [&](const hippt::Bvh4 &b) {
-            return hippt::mesh_lds_bytes(0, int(b.nodes.size() / hippt::kNode4Words), numSlots, true, 0,
+            return hippt::mesh_lds_bytes(0, int(b.nodes.size() / hippt::kNode4Words), numPrims, true, 0,
                                          numMaterials) <= hippt::mesh_lds_scene_limit();
         };
         if (fits(bvh4)) {
@@ -1084,13 +1073,10 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
     byte_codes(sc.nodes4q, hippt::kNode4QWords, 12, hippt::kNode4QWords * 4);
     sc.levels4 = bvh4.levels;
     sc.stackBound4 = bvh4.stackBound;
-    sc.tris.assign(size_t(numSlots) * 3, float4{});
-    sc.shade.assign(size_t(numSlots), float4{});
-    // 40-byte records: v0, e1, e2, id (10 words); + slack for the over-read of a last 1-primitive leaf
-    std::vector<float> t40(tris40 ? size_t(numSlots) * 10 + 8 : 0, 0.0f);
-    for (int k = 0; k < numSlots; ++k) {
+    sc.tris.assign(size_t(numPrims) * 3, float4{});
+    sc.shade.assign(size_t(numPrims), float4{});
+    for (int k = 0; k < numPrims; ++k) {
         const int id = bvh.order[size_t(k)];
-        if (id < 0) continue;  // padding slot: never referenced by a leaf
         if (id >= numTris) {  // sphere: (center, r) (r^2) (-, id, tag 1); shade (center, mat | flag)
             const float *q = spheres + 4 * size_t(id - numTris);
             sc.tris[3 * size_t(k)] = float4{q[0], q[1], q[2], q[3]};
@@ -1119,14 +1105,7 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
         sc.tris[3 * size_t(k) + 1] = float4{e1[1], e1[2], e2[0], e2[1]};
         sc.tris[3 * size_t(k) + 2] = float4{e2[2], as_float(id), 0.0f, 0.0f};
         sc.shade[size_t(k)] = float4{n[0], n[1], n[2], as_float(triMaterial[id])};
-        if (tris40) {
-            float *r = &t40[10 * size_t(k)];
-            const float rec[10] = {v[0], v[1], v[2], e1[0], e1[1], e1[2], e2[0], e2[1], e2[2], as_float(id)};
-            std::memcpy(r, rec, sizeof(rec));
-        }
     }
-    sc.tris40.assign((t40.size() + 3) / 4, float4{});
-    if (!t40.empty()) std::memcpy(sc.tris40.data(), t40.data(), t40.size() * sizeof(float));
     sc.mats.assign(size_t(numMaterials) * 2, float4{});
     for (int m = 0; m < numMaterials; ++m) {
         const hipptMaterial &mt = materials[m];
@@ -1135,7 +1114,7 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
         sc.mats[2 * size_t(m)] = float4{mt.albedo[0], mt.albedo[1], mt.albedo[2], as_float(mt.kind)};
         sc.mats[2 * size_t(m) + 1] = float4{fuzz, mt.ir, 0.0f, 0.0f};
     }
-    sc.numTris = numSlots;
+    sc.numTris = numPrims;
     sc.numNodes = int(bvh.nodes.size() / hippt::kNodeWords);
     sc.levels = bvh.levels;
     sc.full = full;
@@ -1502,10 +1481,6 @@ extern "C" bool hipptSetOption(int key, long long value) {
         if (value < -1 || value > 1) return false;
         s.fuseCombine = int(value);
         return true;
-    case HIPPT_OPT_TRIS40:
-        if (value != 0 && value != 1) return false;
-        s.tris40 = value == 1;
-        return true;
     default: return false;
     }
 }
@@ -1545,7 +1520,6 @@ extern "C" long long hipptGetOption(int key) {
     case HIPPT_OPT_PIXEL_FORMAT: return s.pixelFormat;
     case HIPPT_OPT_CAMERA_POOL: return s.cameraPool;
     case HIPPT_OPT_FUSE_COMBINE: return s.fuseCombine;
-    case HIPPT_OPT_TRIS40: return s.tris40 ? 1 : 0;
     case HIPPT_INFO_LDS_TOP_BYTES: return s.activeTopBytes;
     case HIPPT_INFO_BLOCKS_PER_CU: return s.activeBlocksPerCu;
     default: return -1;

@@ -82,10 +82,6 @@ struct MeshParams {
     // LDS-resident 4-wide trees: low bits of a packed child key that carry the child's code
     // (trace::child_key_p; hippt_api.cpp packed_ref_bits)
     unsigned refBits;
-    // Lambertian triangle scenes (null otherwise): 40-byte triangle records v0, e1, e2, id at
-    // byte 40*i for primitive slot i; every leaf starts at an even slot, so a pair of triangles
-    // is five 16-byte-aligned float4 loads (trace::leaf_step TRI40)
-    const float4 *tris40;
     // random_in_unit_sphere memoized (null: the rejection loop): entry 2^32-word table, see
     // launch_rng_table
     const uint32_t *rngTable;

@@ -461,8 +461,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
             prof<STATS>(pc, 2);
             if (WIDE)
                 traverse_round_wide<nodeF4, STATS, FULL, QUANT, SPILL, LDS_SCENE, TOP, HYBRID, PACKED>(
-                    T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit, S, P.topBytes, P.refBits,
-                    LDS_SCENE ? nullptr : P.tris40);
+                    T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit, S, P.topBytes, P.refBits);
             else
                 traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
         } while (__popcll(__ballot(busy(T))) > unsigned(P.waveThreshold));

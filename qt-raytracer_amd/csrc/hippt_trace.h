@@ -14,12 +14,6 @@
 
 #pragma clang fp contract(off)
 
-// Lambertian triangle scenes read from global memory take their triangles from the 40-byte records
-// (MeshParams::tris40) when present: 0 keeps the 48-byte records everywhere (A/B builds)
-#ifndef HIPPT_TRI40
-#define HIPPT_TRI40 1
-#endif
-
 namespace hippt {
 namespace trace {
 
@@ -593,29 +587,10 @@ __device__ __forceinline__ void test_prim(Trav &T, const Ray &r, const float4 *t
 // so that lanes with short leaves move on: Cornell -9%, blob70k -5%.)
 template <bool STATS, bool FULL, typename Pop, bool PAIRS = false>
 __device__ __forceinline__ void leaf_step(Trav &T, const Ray &r, const float4 *tris, unsigned long long &ntest,
-                                          unsigned *pc, Pop pop, const float4 *tris40 = nullptr) {
+                                          unsigned *pc, Pop pop) {
     const int code = ~T.leaf;
     const int first = code >> 4, last = first + (code & 15);
-    if (PAIRS && !FULL && HIPPT_TRI40 && tris40) {
-        // 40-byte records (v0, e1, e2, id), every leaf at an even slot: a pair of triangles is the five
-        // float4 at byte 40*i (one load fewer than two 48-byte records); a lone last triangle three
-        // (the third over-reads the next record, which exists or is slack)
-        for (int i = first; i < last; i += 2) {
-            const float4 *tp = reinterpret_cast<const float4 *>(reinterpret_cast<const char *>(tris40) + size_t(i) * 40);
-            const float4 L0 = tp[0], L1 = tp[1], L2 = tp[2];
-            const bool two = i + 1 < last;
-            float4 L3 = L0, L4 = L1;
-            if (two) {
-                L3 = tp[3];
-                L4 = tp[4];
-            }
-            test_prim_data<STATS, FULL>(T, r, L0, L1, make_float4(L2.x, L2.y, 0.0f, 0.0f), i, ntest, pc);
-            if (two)
-                test_prim_data<STATS, FULL>(T, r, make_float4(L2.z, L2.w, L3.x, L3.y),
-                                            make_float4(L3.z, L3.w, L4.x, L4.y), make_float4(L4.z, L4.w, 0.0f, 0.0f),
-                                            i + 1, ntest, pc);
-        }
-    } else if (PAIRS) {
+    if (PAIRS) {
         // two primitives' loads in flight per iteration (trees in global memory: blob70k +3%;
         // no gain from LDS)
         for (int i = first; i < last; i += 2) {
@@ -849,8 +824,7 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
                                                     const float4 *tris, unsigned long long &nvis,
                                                     unsigned long long &ntest, unsigned *pc, unsigned leafExit,
                                                     unsigned nodeExit, const SpillArea &S,
-                                                    unsigned topBytes = 0, unsigned refBits = 0,
-                                                    const float4 *tris40 = nullptr) {
+                                                    unsigned topBytes = 0, unsigned refBits = 0) {
     static_assert(!HYBRID || (QUANT && TOP), "hybrid trees: 8-bit nodes below an LDS top");
     static_assert(!PACKED || (LDS0 && !QUANT), "packed keys: LDS-resident float trees");
     const unsigned refMask = PACKED ? (1u << refBits) - 1u : 0u;
@@ -977,7 +951,7 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
     auto popw = [&] { return pop_wide<SPILL, PACKED>(T, my, S, refBits); };
     while (T.leaf != 0) {
         prof<STATS>(pc, 4);
-        leaf_step<STATS, FULL, decltype(popw), !LDS0>(T, r, tris, ntest, pc, popw, tris40);
+        leaf_step<STATS, FULL, decltype(popw), !LDS0>(T, r, tris, ntest, pc, popw);
         if (nodeExit && __popcll(__ballot(T.leaf != 0)) <= nodeExit) break;
     }
 }

@@ -187,8 +187,7 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
         do {
             if (WIDE)
                 traverse_round_wide<nodeF4, STATS, FULL, QUANT, true, LDS_SCENE, TOP>(
-                    T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit, S, P.topBytes, 0u,
-                    LDS_SCENE ? nullptr : P.tris40);
+                    T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit, S, P.topBytes);
             else
                 traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
         } while (__popcll(__ballot(busy(T))) > unsigned(P.waveThreshold));

@@ -68,7 +68,7 @@ def pt():
     t.useBuiltinScene(hippt.SCENE_SPHERE4)
     yield t
     for k, v in ((hippt.OPT_LDS_SCENE, 1), (hippt.OPT_BVH_WIDTH, 0), (hippt.OPT_PATH_MODE, 0),
-                 (hippt.OPT_WAVEFRONT_SLOTS, 1 << 24), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_TRIS40, 1)):
+                 (hippt.OPT_WAVEFRONT_SLOTS, 1 << 24), (hippt.OPT_BVH_QUANT, -1)):
         t.setOption(k, v)
     hippt.load_library().cudaPathTracerShutdown()
 
@@ -79,9 +79,7 @@ MODES = {
     "wide2": ((hippt.OPT_LDS_SCENE, 0), (hippt.OPT_BVH_WIDTH, 2), (hippt.OPT_PATH_MODE, 0)),
     "quant8": ((hippt.OPT_LDS_SCENE, 0), (hippt.OPT_BVH_WIDTH, 0), (hippt.OPT_BVH_QUANT, 1)),
     "hybrid": ((hippt.OPT_LDS_SCENE, 0), (hippt.OPT_BVH_WIDTH, 0), (hippt.OPT_BVH_QUANT, 2)),
-    # 48-byte triangle records only (no leaf padding): HIPPT_OPT_TRIS40 0, the other modes use 1
-    "tris48": ((hippt.OPT_LDS_SCENE, 0), (hippt.OPT_BVH_WIDTH, 0), (hippt.OPT_BVH_QUANT, 0), (hippt.OPT_TRIS40, 0)),
-    "wavefront": ((hippt.OPT_LDS_SCENE, 1), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_PATH_MODE, 1), (hippt.OPT_TRIS40, 1),
+    "wavefront": ((hippt.OPT_LDS_SCENE, 1), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_PATH_MODE, 1),
                   (hippt.OPT_WAVEFRONT_SLOTS, 500)),
 }
 

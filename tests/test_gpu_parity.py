@@ -30,7 +30,7 @@ def pt():
                  (hippt.OPT_STACK_CAP, 0), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_LDS_TOP_NODES, -1),
                  (hippt.OPT_RNG_TABLE, 0), (hippt.OPT_BVH_COLLAPSE, -1), (hippt.OPT_BVH_NODE_COST, 200),
                  (hippt.OPT_BVH_LEAF4, 4), (hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_ARGB),
-                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1), (hippt.OPT_TRIS40, 1)):
+                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1)):
         t.setOption(k, v)
     t.resetStats()
     yield t
@@ -490,32 +490,6 @@ def test_mesh_batches_and_frame_splits_are_bit_identical(pt):
         assert pt.renderFrames(n, 8)
     split = pt.readback()
     _assert_same(one[0], one[1], split[0], split[1])
-
-
-@pytest.mark.parametrize("name", ["blob70k", "cloud180"])
-def test_triangle_record_layouts_do_not_change_results(pt, name):
-    """Lambertian triangle scenes read from global memory: leaves padded to even slots with the
-    40-byte records (a 2-triangle leaf in 5 loads; HIPPT_OPT_TRIS40 1, the default) and the
-    48-byte records without padding (0), over float, 8-bit and 2-wide trees and the wavefront:
-    the oracle's image bit for bit, counts included."""
-    sc = scenes.cloud_scene(180) if name == "cloud180" else scenes.get_scene(name)
-    w, h = 52, 36
-    ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
-    pt.setOption(hippt.OPT_LDS_SCENE, 0)
-    for t40 in (1, 0):
-        pt.setOption(hippt.OPT_TRIS40, t40)
-        pt.uploadMesh(sc)
-        for width, quant, mode in ((0, 0, 0), (0, 1, 0), (2, -1, 0), (0, -1, 1)):
-            pt.setOption(hippt.OPT_BVH_WIDTH, width)
-            pt.setOption(hippt.OPT_BVH_QUANT, quant)
-            pt.setOption(hippt.OPT_PATH_MODE, mode)
-            assert pt.initialize(w, h)
-            pt.resetStats()
-            assert pt.renderFrames(3, 8)
-            got = pt.readback()
-            _assert_same(got[0], got[1], ora[0], ora[1])
-            st = pt.stats()
-            assert st["segments"] == ora[2] and st["pixelSamples"] == ora[3]
 
 
 @pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene"])
