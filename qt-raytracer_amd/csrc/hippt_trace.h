@@ -816,7 +816,10 @@ __device__ __forceinline__ void cas_key(unsigned &ka, unsigned &kb) {
 // every ray makes at the top of the tree.
 // HYBRID (with QUANT and TOP; bvh_builder.h hybrid_bvh4): the top is 128-byte float nodes (read
 // from LDS, no decode) and every node below it a 64-byte 8-bit node in global memory (4 loads
-// instead of 7 where the TA binds); a node byte offset below topBytes is a top node.
+// instead of 7 where the TA binds); a node byte offset below topBytes is a top node.  Top first:
+// an iteration in which any lane is at a top node visits only those lanes' nodes (the float path),
+// the others wait; otherwise every lane visits its 8-bit node.  The two paths never run in the
+// same iteration (run together under divergence they cost both paths' VALU: 17.5 vs 20.9 G).
 // PACKED (LDS-resident scenes): packed child keys (pack_key), refBits low bits carrying the code.
 template <int NODE_F4, bool STATS, bool FULL, bool QUANT = false, bool SPILL = true, bool LDS0 = false,
           bool TOP = false, bool HYBRID = false, bool PACKED = false>
@@ -837,10 +840,14 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
         // byte offsets from the uniform base: base-register + offset-register loads).  NODE_F4
         // (the node stride) is implied by the codes: the device trees store byte offsets.
         const unsigned nb = unsigned(T.cur);  // interior codes are node byte offsets
+        const bool topVisit = TOP && nb < topBytes;
+        // HYBRID: a wave-uniform choice of the node format visited this iteration
+        const bool topIter = HYBRID && __ballot(topVisit) != 0;
+        // below the top while other lanes are at it: this lane waits (the exit test still counts it)
+        if (!(HYBRID && topIter && !topVisit)) {
         unsigned k0, k1, k2, k3;
         int4 ch;
-        const bool topVisit = TOP && nb < topBytes;
-        if (!QUANT || (HYBRID && topVisit)) {
+        if (!QUANT || (HYBRID && topIter)) {
             // 128-byte float nodes (LDS and global): nb's low 7 bits are zero, so the octant's
             // near row is nb | s and the far row its ^ 16
             const unsigned ax = nb | sx, ay = nb | sy, az = nb | sz;
@@ -946,6 +953,7 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
             T.leaf = T.cur;
             T.cur = pop_wide<SPILL, PACKED>(T, my, S, refBits);
         }
+        }  // visiting lanes
         if (__popcll(__ballot((T.leaf | T.cur) >= 0)) <= leafExit) break;
     }
     auto popw = [&] { return pop_wide<SPILL, PACKED>(T, my, S, refBits); };
