@@ -391,7 +391,25 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                     need = false;
                     pool_take<POOL>(P, pool, poolNext + rank, item, r, rng);
                 }
-                if (n > avail) {
+                if (HIPPT_EXACT_TAIL && n > avail && Q.tail) {
+                    // the queue's tail: no pool of claimed items beyond what the lanes need now (a
+                    // pool held while other waves idle lengthens the launch's tail); the lanes the
+                    // pool's rest did not serve claim and generate their own
+                    poolNext = 64;
+                    const unsigned it = queue_fetch(need, Q, P.queue, P.totalItems, P.chunk);
+#ifdef HIPPT_DEBUG_TIMELINE
+                    if (!tlDrained && __ballot(need && it == kNone)) tlDrained = __builtin_amdgcn_s_memrealtime();
+                    tlItems += __popcll(__ballot(need && it != kNone));
+#endif
+                    if (need) {
+                        need = false;
+                        item = it;
+                        if (it != kNone) {
+                            prof<STATS>(pc, 1);
+                            camera_sample(P, it, r, rng);
+                        }
+                    }
+                } else if (n > avail) {
                     // the camera rays of the wave's next 64 items, every lane at once
                     const unsigned it = queue_fetch(true, Q, P.queue, P.totalItems, P.chunk);
 #ifdef HIPPT_DEBUG_TIMELINE

@@ -139,15 +139,22 @@ __device__ __forceinline__ unsigned wave_fetch(bool req, unsigned &poolNext, uns
 // into kQueues contiguous queues, one per XCD (block b is dispatched to XCD b % 8), each with
 // its counter on its own 128-byte line (queue[g * kQueueStride]).  A wave's first chunk is
 // assigned statically (no atomic at kernel start, where all waves would contend), further
-// chunks come from its home queue's counter, chunks shrink to kTailChunk items once the queue
-// is within one chunk per wave of its end (a short tail), and a wave whose home queue is
-// drained moves on to the others.  Counters start at 0 and count dynamically claimed items.
+// chunks come from its home queue's counter, and a wave whose home queue is drained moves on to
+// the others.  Once a queue is within one chunk per wave of its end, a wave claims exactly the
+// items its requesting lanes need (HIPPT_EXACT_TAIL; before round 3: 64-item chunks): claimed
+// items a wave holds while other waves idle are what made the launch's tail (the per-wave
+// timeline of a 1/8 share: waves found the queues empty over a 258 µs spread).  Counters start at
+// 0 and count dynamically claimed items.
+#ifndef HIPPT_EXACT_TAIL
+#define HIPPT_EXACT_TAIL 1
+#endif
 constexpr unsigned kQueues = 8, kQueueStride = 32, kTailChunk = 64;
 
 struct WorkQueue {
     unsigned g, left;  // current queue, queues not yet found drained
     unsigned next, end;  // this wave's pool [next, end) (all items of queue g)
     unsigned qEnd, dynBase, waves;  // queue g: end, first dynamically claimed item, home waves
+    bool tail;  // a claim of this wave has been a tail claim (wave-uniform)
 };
 
 __device__ __forceinline__ unsigned queue_start(unsigned total, unsigned g) {
@@ -162,6 +169,7 @@ __device__ __forceinline__ void queue_select(WorkQueue &Q, unsigned g, unsigned 
 }
 
 __device__ __forceinline__ void queue_begin(WorkQueue &Q, unsigned total, unsigned chunk) {
+    Q.tail = false;
     queue_select(Q, blockIdx.x % kQueues, total, chunk);
     Q.left = kQueues;
     const unsigned wid = (blockIdx.x / kQueues) * 4u + (threadIdx.x >> 6);
@@ -186,7 +194,9 @@ __device__ __forceinline__ unsigned queue_fetch(bool req, WorkQueue &Q, unsigned
     while (Q.left && __ballot(want)) {
         m = __ballot(want);
         rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
-        const unsigned c = Q.qEnd - min(Q.end, Q.qEnd) < Q.waves * chunk ? kTailChunk : chunk;
+        const bool tail = Q.qEnd - min(Q.end, Q.qEnd) < Q.waves * chunk;
+        Q.tail = Q.tail || tail;
+        const unsigned c = !tail ? chunk : HIPPT_EXACT_TAIL ? unsigned(__popcll(m)) : kTailChunk;
         unsigned base = 0;
         if (__lane_id() == 0) base = atomicAdd(&ctr[Q.g * kQueueStride], c);
         base = __builtin_amdgcn_readfirstlane(base) + Q.dynBase;
@@ -816,10 +826,10 @@ __device__ __forceinline__ void cas_key(unsigned &ka, unsigned &kb) {
 // every ray makes at the top of the tree.
 // HYBRID (with QUANT and TOP; bvh_builder.h hybrid_bvh4): the top is 128-byte float nodes (read
 // from LDS, no decode) and every node below it a 64-byte 8-bit node in global memory (4 loads
-// instead of 7 where the TA binds); a node byte offset below topBytes is a top node.  Top first:
-// an iteration in which any lane is at a top node visits only those lanes' nodes (the float path),
-// the others wait; otherwise every lane visits its 8-bit node.  The two paths never run in the
-// same iteration (run together under divergence they cost both paths' VALU: 17.5 vs 20.9 G).
+// instead of 7 where the TA binds); a node byte offset below topBytes is a top node.  Measured and
+// kept off: the wave's lanes straddle the top/bottom boundary on most iterations,
+// which then run both paths (blob70k 17.5 vs 20.9 G); visiting the top first, the lanes below it
+// waiting, was worse still (11.7 G).
 // PACKED (LDS-resident scenes): packed child keys (pack_key), refBits low bits carrying the code.
 template <int NODE_F4, bool STATS, bool FULL, bool QUANT = false, bool SPILL = true, bool LDS0 = false,
           bool TOP = false, bool HYBRID = false, bool PACKED = false>
@@ -841,13 +851,9 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
         // (the node stride) is implied by the codes: the device trees store byte offsets.
         const unsigned nb = unsigned(T.cur);  // interior codes are node byte offsets
         const bool topVisit = TOP && nb < topBytes;
-        // HYBRID: a wave-uniform choice of the node format visited this iteration
-        const bool topIter = HYBRID && __ballot(topVisit) != 0;
-        // below the top while other lanes are at it: this lane waits (the exit test still counts it)
-        if (!(HYBRID && topIter && !topVisit)) {
         unsigned k0, k1, k2, k3;
         int4 ch;
-        if (!QUANT || (HYBRID && topIter)) {
+        if (!QUANT || (HYBRID && topVisit)) {
             // 128-byte float nodes (LDS and global): nb's low 7 bits are zero, so the octant's
             // near row is nb | s and the far row its ^ 16
             const unsigned ax = nb | sx, ay = nb | sy, az = nb | sz;
@@ -953,7 +959,6 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
             T.leaf = T.cur;
             T.cur = pop_wide<SPILL, PACKED>(T, my, S, refBits);
         }
-        }  // visiting lanes
         if (__popcll(__ballot((T.leaf | T.cur) >= 0)) <= leafExit) break;
     }
     auto popw = [&] { return pop_wide<SPILL, PACKED>(T, my, S, refBits); };
