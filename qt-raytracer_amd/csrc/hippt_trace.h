@@ -154,8 +154,12 @@ struct WorkQueue {
     unsigned g, left;  // current queue, queues not yet found drained
     unsigned next, end;  // this wave's pool [next, end) (all items of queue g)
     unsigned qEnd, dynBase, waves;  // queue g: end, first dynamically claimed item, home waves
-    bool tail;  // a claim of this wave has been a tail claim (wave-uniform)
 };
+
+// Queue g is within one chunk per home wave of its end: claims are exact from here on.
+__device__ __forceinline__ bool queue_tail(const WorkQueue &Q, unsigned chunk) {
+    return Q.qEnd - min(Q.end, Q.qEnd) < Q.waves * chunk;
+}
 
 __device__ __forceinline__ unsigned queue_start(unsigned total, unsigned g) {
     return unsigned((unsigned long long)total * g / kQueues);
@@ -169,7 +173,6 @@ __device__ __forceinline__ void queue_select(WorkQueue &Q, unsigned g, unsigned 
 }
 
 __device__ __forceinline__ void queue_begin(WorkQueue &Q, unsigned total, unsigned chunk) {
-    Q.tail = false;
     queue_select(Q, blockIdx.x % kQueues, total, chunk);
     Q.left = kQueues;
     const unsigned wid = (blockIdx.x / kQueues) * 4u + (threadIdx.x >> 6);
@@ -194,9 +197,7 @@ __device__ __forceinline__ unsigned queue_fetch(bool req, WorkQueue &Q, unsigned
     while (Q.left && __ballot(want)) {
         m = __ballot(want);
         rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
-        const bool tail = Q.qEnd - min(Q.end, Q.qEnd) < Q.waves * chunk;
-        Q.tail = Q.tail || tail;
-        const unsigned c = !tail ? chunk : HIPPT_EXACT_TAIL ? unsigned(__popcll(m)) : kTailChunk;
+        const unsigned c = !queue_tail(Q, chunk) ? chunk : HIPPT_EXACT_TAIL ? unsigned(__popcll(m)) : kTailChunk;
         unsigned base = 0;
         if (__lane_id() == 0) base = atomicAdd(&ctr[Q.g * kQueueStride], c);
         base = __builtin_amdgcn_readfirstlane(base) + Q.dynBase;
