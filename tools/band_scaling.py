@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--all-bands", action="store_true", help="time every rank's rows (max = the N-GPU step)")
     ap.add_argument("--split", default="interleave", choices=["interleave", "bands"])
+    ap.add_argument("opts", nargs="*", help="KEY=VALUE hipptSetOption pairs (numeric keys)")
     a = ap.parse_args()
     sc = scenes.get_scene(a.scene)
     full_ms = None
@@ -35,6 +36,9 @@ def main():
     for n, rank in jobs:
         pt = hippt.PathTracer()
         pt.setDevices([0])
+        for o in a.opts:
+            k, v = o.split("=")
+            pt.setOption(int(k), int(v))
         if a.split == "interleave":
             pt.setRowInterleave(rank, n)
             nrows = len(range(rank, a.height, n))
