@@ -110,8 +110,6 @@ def parse():
     p.add_argument("--scratch-mb", type=int, default=None)
     p.add_argument("--bvh-width", type=int, default=None, choices=[0, 2, 4],
                    help="megakernel BVH width (HIPPT_OPT_BVH_WIDTH; default automatic)")
-    p.add_argument("--trace-streams", type=int, default=None, choices=[0, 1],
-                   help="HIPPT_OPT_TRACE_STREAMS: overlapped batches on two trace streams (default: the library's)")
     p.add_argument("--cpu-baseline", default="auto", choices=["auto", "reference", "port", "off"])
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="target duration of one CPU sample run")
     p.add_argument("--cpu-runs", type=int, default=3, help="CPU sample runs (the median is reported)")
@@ -339,8 +337,6 @@ def main():
         pt.setOption(hippt.OPT_SCRATCH_MB, args.scratch_mb)
     if args.bvh_width is not None:
         pt.setOption(hippt.OPT_BVH_WIDTH, args.bvh_width)
-    if args.trace_streams is not None:
-        pt.setOption(hippt.OPT_TRACE_STREAMS, args.trace_streams)
     pt.setOption(hippt.OPT_PATH_MODE, 1 if args.path_mode == "wavefront" else 0)
     if args.wavefront_slots is not None:
         pt.setOption(hippt.OPT_WAVEFRONT_SLOTS, args.wavefront_slots)

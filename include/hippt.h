@@ -231,11 +231,6 @@ enum {
                                        batch's launch on the same device (beside its paths) instead of as a
                                        launch of its own, whenever nothing reads the image in between (1), or
                                        never (0); -1 (default): automatic.  Same results either way */
-    , HIPPT_OPT_TRACE_STREAMS = 29  /* megakernel: consecutive batches trace on two streams, each into its own
-                                       scratch, and are combined in order on the context's stream, so a batch
-                                       starts on the SIMDs its predecessor's tail leaves idle (1), or one
-                                       stream with the combine fused into the next launch (0, default).  Same
-                                       results either way */
 };
 /* Output frame word formats (HIPPT_OPT_PIXEL_FORMAT).  Both map an accumulated colour c to
  * sqrt(clamp(c, 0, 1)) per channel.

@@ -57,22 +57,6 @@ struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
 };
 
-// Overlapped megakernel batches (HIPPT_OPT_TRACE_STREAMS): consecutive batches trace on two
-// streams, each into a slot of its own (per-sample scratch, work-queue counters, spill area), and
-// the main stream runs their combines in batch order.  A batch's persistent grid then starts on
-// the SIMDs its predecessor's tail leaves idle (the last in-flight paths finishing at falling SIMD
-// efficiency: ~0.3 ms per launch on Cornell, ~1 ms on blob70k).
-constexpr int kTraceSlots = 3;
-struct TraceSlot {
-    float *scratch = nullptr;
-    size_t scratchBytes = 0;
-    unsigned *queue = nullptr;
-    int *spill = nullptr;
-    size_t spillBytes = 0;
-    hipEvent_t traceDone = nullptr, combineDone = nullptr;
-    bool used = false;  // combineDone recorded
-};
-
 struct Ctx {
     int device = 0;
     int y0 = 0, rows = 0, stride = 1;  // image rows y0, y0+stride, ... (rows of them)
@@ -115,10 +99,6 @@ struct Ctx {
     std::vector<EventPair> freeEv;                       // pairs not in flight
     std::vector<std::pair<int, EventPair>> pending;      // (0 trace / 1 combine, events)
     hipEvent_t presentEv[2] = {nullptr, nullptr};        // band copy into State::present[b] done
-    hipStream_t traceStream[2] = {nullptr, nullptr};     // overlapped batches (HIPPT_OPT_TRACE_STREAMS)
-    TraceSlot slots[kTraceSlots];
-    int nextSlot = 0;
-    long long batchSeq = 0;
 };
 
 struct SceneHost {
@@ -177,7 +157,6 @@ struct State {
     int pixelFormat = HIPPT_PIXEL_ARGB;  // output frame words (HIPPT_OPT_PIXEL_FORMAT)
     int cameraPool = -1;  // megakernel camera-ray pool (HIPPT_OPT_CAMERA_POOL; -1: automatic)
     int fuseCombine = -1;  // combine inside the next megakernel launch (HIPPT_OPT_FUSE_COMBINE)
-    int traceStreams = 0;  // overlapped megakernel batches on two trace streams (HIPPT_OPT_TRACE_STREAMS)
     std::vector<std::pair<int, uint32_t *>> rngTables;  // per device, built on first use
     unsigned activeTopBytes = 0;  // of the last mesh render (hipptGetOption HIPPT_INFO_*)
     int activeBlocksPerCu = 0;
@@ -306,18 +285,6 @@ void destroy_ctx(Ctx &c) {
     }
     for (hipEvent_t e : c.presentEv)
         if (e) (void)hipEventDestroy(e);
-    for (hipStream_t &t : c.traceStream)
-        if (t) {
-            (void)hipStreamSynchronize(t);
-            (void)hipStreamDestroy(t);
-        }
-    for (TraceSlot &sl : c.slots) {
-        (void)hipFree(sl.scratch);
-        (void)hipFree(sl.queue);
-        (void)hipFree(sl.spill);
-        if (sl.traceDone) (void)hipEventDestroy(sl.traceDone);
-        if (sl.combineDone) (void)hipEventDestroy(sl.combineDone);
-    }
     if (c.stream) (void)hipStreamDestroy(c.stream);
     c = Ctx();
 }
@@ -388,9 +355,6 @@ bool harvest_locked(Ctx &c, const char **err) {
 bool ensure_scene(Ctx &c, const char **err) {
     State &s = S();
     if (s.scene.kind != HIPPT_SCENE_MESH || c.sceneVersion == s.scene.version) return true;
-    // batches still tracing the old scene on a trace stream: the main stream waits for every trace
-    // (each is combined on it)
-    HIP_TRY(hipStreamSynchronize(c.stream));
     free_scene_buffers(c);
     auto up = [&](float4 *&dst, const std::vector<float4> &src) -> bool {
         HIP_TRY(hipMalloc(&dst, std::max<size_t>(16, src.size() * sizeof(float4))));
@@ -528,35 +492,6 @@ bool ensure_spill(Ctx &c, hippt::MeshParams &p, long long blocks, bool spills, i
         c.spillBytes = bytes;
     }
     p.spill = c.spill;
-    return true;
-}
-
-// A trace slot's buffers for a batch: scratch of `need` bytes, work-queue counters, and (trees that
-// spill) the per-lane spill area of a `blocks`-block grid.  Growing a buffer waits for the slot's
-// previous batch to be combined.
-bool slot_buffers(Ctx &c, TraceSlot &sl, size_t need, long long blocks, bool spills, int spillCap,
-                  const char **err) {
-    const size_t spillBytes = spills ? size_t(blocks) * hippt::kMeshBlock * size_t(spillCap) * sizeof(int) : 0;
-    if (!sl.traceDone) {
-        HIP_TRY(hipEventCreateWithFlags(&sl.traceDone, hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&sl.combineDone, hipEventDisableTiming));
-    }
-    if ((sl.scratchBytes < need || sl.spillBytes < spillBytes) && sl.used) HIP_TRY(hipEventSynchronize(sl.combineDone));
-    if (sl.scratchBytes < need) {
-        (void)hipFree(sl.scratch);
-        sl.scratch = nullptr;
-        sl.scratchBytes = 0;
-        HIP_TRY(hipMalloc(&sl.scratch, need));
-        sl.scratchBytes = need;
-    }
-    if (sl.spillBytes < spillBytes) {
-        (void)hipFree(sl.spill);
-        sl.spill = nullptr;
-        sl.spillBytes = 0;
-        HIP_TRY(hipMalloc(&sl.spill, spillBytes));
-        sl.spillBytes = spillBytes;
-    }
-    if (!sl.queue) HIP_TRY(hipMalloc(&sl.queue, kQueueBytes));
     return true;
 }
 
@@ -864,11 +799,10 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                     const int nf = std::min(fpb, count - b);
                     const unsigned total = bandPixels * unsigned(nf);
                     // the megakernel takes the previous batch's combine along; other batches flush it
-                    const bool overlap = maxDepth > 0 && s.pathMode == 0 && s.traceStreams != 0;
-                    const bool fuse = !overlap && maxDepth > 0 && s.pathMode == 0 && s.fuseCombine != 0;
+                    const bool fuse = maxDepth > 0 && s.pathMode == 0 && s.fuseCombine != 0;
                     if (!fuse && !flush_deferred(c, err)) return false;
                     float *scratch = nullptr;
-                    if (!overlap && !batch_scratch(c, need, &scratch, err)) return false;
+                    if (!batch_scratch(c, need, &scratch, err)) return false;
                     if (maxDepth <= 0) {
                         // ray_color with depth <= 0 returns black without tracing (RayTracer.h:582-583)
                         HIP_TRY(hipMemsetAsync(scratch, 0, size_t(total) * 3 * sizeof(float), c.stream));
@@ -927,41 +861,6 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         if (s.rngTable && !rng_table(c, &p.rngTable, err)) return false;
                         if (s.pathMode == 1) {
                             if (!run_wavefront(c, p, cnt, spills, s.scene.stackBound4 + 3, err)) return false;
-                        } else if (overlap) {
-                            // overlapped batches: this batch traces on its own stream into its own slot
-                            // (after the slot's previous batch has been combined); the main stream
-                            // combines it after its trace, in batch order
-                            long long blocks = (long long)c.cus * bpc;
-                            blocks = std::min<long long>(blocks, (total + hippt::kMeshBlock - 1) / hippt::kMeshBlock);
-                            blocks = std::max<long long>(blocks, 1);
-                            TraceSlot &sl = c.slots[c.nextSlot];
-                            c.nextSlot = (c.nextSlot + 1) % kTraceSlots;
-                            hipStream_t &ts = c.traceStream[c.batchSeq++ & 1];
-                            if (!ts) HIP_TRY(hipStreamCreateWithFlags(&ts, hipStreamNonBlocking));
-                            const int spillCap = s.scene.stackBound4 + 3;
-                            if (!slot_buffers(c, sl, need, blocks, spills, spillCap, err)) return false;
-                            if (sl.used) HIP_TRY(hipStreamWaitEvent(ts, sl.combineDone, 0));
-                            p.scratch = sl.scratch;
-                            p.queue = sl.queue;
-                            p.combCtr = sl.queue + kCombCtrWord;
-                            p.spillCap = spillCap;
-                            p.spill = spills ? sl.spill : nullptr;
-                            HIP_TRY(hipMemsetAsync(sl.queue, 0, kQueueBytes, ts));
-                            EventPair ev;
-                            if (!next_events(c, ev, err)) return false;
-                            HIP_TRY(hipEventRecord(ev.a, ts));
-                            HIP_TRY(hippt::launch_mesh(p, int(blocks), cnt, ts));
-                            HIP_TRY(hipEventRecord(ev.b, ts));
-                            c.pending.push_back({0, ev});
-                            HIP_TRY(hipEventRecord(sl.traceDone, ts));
-                            HIP_TRY(hipStreamWaitEvent(c.stream, sl.traceDone, 0));
-                            c.deferred = hippt::CombineParams{c.accum, c.out, sl.scratch, bandPixels, total,
-                                                              firstFrame + b, nf, s.pixelFormat};
-                            c.hasDeferred = true;
-                            if (!flush_deferred(c, err)) return false;
-                            HIP_TRY(hipEventRecord(sl.combineDone, c.stream));
-                            sl.used = true;
-                            continue;
                         } else {
                             long long blocks = (long long)c.cus * bpc;
                             blocks = std::min<long long>(blocks, (total + hippt::kMeshBlock - 1) / hippt::kMeshBlock);
@@ -1582,10 +1481,6 @@ extern "C" bool hipptSetOption(int key, long long value) {
         if (value < -1 || value > 1) return false;
         s.fuseCombine = int(value);
         return true;
-    case HIPPT_OPT_TRACE_STREAMS:
-        if (value != 0 && value != 1) return false;
-        s.traceStreams = int(value);
-        return true;
     default: return false;
     }
 }
@@ -1625,7 +1520,6 @@ extern "C" long long hipptGetOption(int key) {
     case HIPPT_OPT_PIXEL_FORMAT: return s.pixelFormat;
     case HIPPT_OPT_CAMERA_POOL: return s.cameraPool;
     case HIPPT_OPT_FUSE_COMBINE: return s.fuseCombine;
-    case HIPPT_OPT_TRACE_STREAMS: return s.traceStreams;
     case HIPPT_INFO_LDS_TOP_BYTES: return s.activeTopBytes;
     case HIPPT_INFO_BLOCKS_PER_CU: return s.activeBlocksPerCu;
     default: return -1;

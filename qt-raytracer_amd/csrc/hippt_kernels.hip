@@ -206,11 +206,6 @@ __device__ unsigned long long g_timeline[65536 * 6];
 #define HIPPT_PACKED_KEYS 1
 #endif
 
-// loop exits off for waves with few live lanes in the launch's tail (see mesh_kernel)
-#ifndef HIPPT_TAIL_SCALE
-#define HIPPT_TAIL_SCALE 1
-#endif
-
 #ifndef HIPPT_WIDE_WAVES_PER_EU
 #define HIPPT_WIDE_WAVES_PER_EU 7
 #endif
@@ -397,9 +392,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                     pool_take<POOL>(P, pool, poolNext + rank, item, r, rng);
                 }
                 if (n > avail) {
-                    // the camera rays of the wave's next 64 items, every lane at once.  (Claiming only
-                    // what the lanes need in the queue's tail, instead of a pool's worth, spilled
-                    // registers in this kernel: measured and not kept)
+                    // the camera rays of the wave's next 64 items, every lane at once
                     const unsigned it = queue_fetch(true, Q, P.queue, P.totalItems, P.chunk);
 #ifdef HIPPT_DEBUG_TIMELINE
                     if (!tlDrained && __ballot(it == kNone)) tlDrained = __builtin_amdgcn_s_memrealtime();
@@ -463,24 +456,16 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         }
         if (!__any(busy(T) || pend != 0u)) break;
 
-        // Loop-exit thresholds are lane counts tuned for a full wave.  In the launch's tail (the
-        // queue drained, paths ending one by one) a wave with few live paths would leave the node
-        // loop, the leaf loop and the traversal after every visit (leafExit 17 > live lanes) and
-        // pay the outer loop per node: below 32 live lanes the exits are off (HIPPT_TAIL_SCALE).
-        const unsigned exitMask =
-            HIPPT_TAIL_SCALE && __popcll(__ballot(item != kNone)) < 32 ? 0u : ~0u;
-        const unsigned leafExit = P.leafExit & exitMask, nodeExit = P.nodeExit & exitMask;
-        const unsigned waveThreshold = unsigned(P.waveThreshold) & exitMask;
 
         // ---- traversal: while-while over the BVH; leave once few lanes remain -------------
         if (!CAP || __any(busy(T))) do {
             prof<STATS>(pc, 2);
             if (WIDE)
                 traverse_round_wide<nodeF4, STATS, FULL, QUANT, SPILL, LDS_SCENE, TOP, HYBRID, PACKED>(
-                    T, r, my, nodes, tris, nvis, ntest, pc, leafExit, nodeExit, S, P.topBytes, P.refBits);
+                    T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit, S, P.topBytes, P.refBits);
             else
-                traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, leafExit, nodeExit);
-        } while (__popcll(__ballot(busy(T))) > waveThreshold);
+                traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
+        } while (__popcll(__ballot(busy(T))) > unsigned(P.waveThreshold));
 
         // ---- shading: lanes whose traversal finished (ray_color step, RayTracer.h:579-596) ----
         if (item != kNone && !busy(T)) {

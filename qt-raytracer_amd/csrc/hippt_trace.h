@@ -139,15 +139,10 @@ __device__ __forceinline__ unsigned wave_fetch(bool req, unsigned &poolNext, uns
 // into kQueues contiguous queues, one per XCD (block b is dispatched to XCD b % 8), each with
 // its counter on its own 128-byte line (queue[g * kQueueStride]).  A wave's first chunk is
 // assigned statically (no atomic at kernel start, where all waves would contend), further
-// chunks come from its home queue's counter, and a wave whose home queue is drained moves on to
-// the others.  Once a queue is within one chunk per wave of its end, a wave claims exactly the
-// items its requesting lanes need (HIPPT_EXACT_TAIL; before round 3: 64-item chunks): claimed
-// items a wave holds while other waves idle are what made the launch's tail (the per-wave
-// timeline of a 1/8 share: waves found the queues empty over a 258 µs spread).  Counters start at
-// 0 and count dynamically claimed items.
-#ifndef HIPPT_EXACT_TAIL
-#define HIPPT_EXACT_TAIL 1
-#endif
+// chunks come from its home queue's counter, chunks shrink to kTailChunk items once the queue
+// is within one chunk per wave of its end (a short tail), and a wave whose home queue is
+// drained moves on to the others.  Counters start at 0 and count dynamically claimed items.
+// (Claiming exactly the requesting lanes' count in the tail instead: neutral)
 constexpr unsigned kQueues = 8, kQueueStride = 32, kTailChunk = 64;
 
 struct WorkQueue {
@@ -155,11 +150,6 @@ struct WorkQueue {
     unsigned next, end;  // this wave's pool [next, end) (all items of queue g)
     unsigned qEnd, dynBase, waves;  // queue g: end, first dynamically claimed item, home waves
 };
-
-// Queue g is within one chunk per home wave of its end: claims are exact from here on.
-__device__ __forceinline__ bool queue_tail(const WorkQueue &Q, unsigned chunk) {
-    return Q.qEnd - min(Q.end, Q.qEnd) < Q.waves * chunk;
-}
 
 __device__ __forceinline__ unsigned queue_start(unsigned total, unsigned g) {
     return unsigned((unsigned long long)total * g / kQueues);
@@ -197,7 +187,7 @@ __device__ __forceinline__ unsigned queue_fetch(bool req, WorkQueue &Q, unsigned
     while (Q.left && __ballot(want)) {
         m = __ballot(want);
         rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
-        const unsigned c = !queue_tail(Q, chunk) ? chunk : HIPPT_EXACT_TAIL ? unsigned(__popcll(m)) : kTailChunk;
+        const unsigned c = Q.qEnd - min(Q.end, Q.qEnd) < Q.waves * chunk ? kTailChunk : chunk;
         unsigned base = 0;
         if (__lane_id() == 0) base = atomicAdd(&ctr[Q.g * kQueueStride], c);
         base = __builtin_amdgcn_readfirstlane(base) + Q.dynBase;

@@ -30,7 +30,7 @@ def pt():
                  (hippt.OPT_STACK_CAP, 0), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_LDS_TOP_NODES, -1),
                  (hippt.OPT_RNG_TABLE, 0), (hippt.OPT_BVH_COLLAPSE, -1), (hippt.OPT_BVH_NODE_COST, 200),
                  (hippt.OPT_BVH_LEAF4, 4), (hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_ARGB),
-                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1), (hippt.OPT_TRACE_STREAMS, 0)):
+                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1)):
         t.setOption(k, v)
     t.resetStats()
     yield t
@@ -492,18 +492,15 @@ def test_mesh_batches_and_frame_splits_are_bit_identical(pt):
     _assert_same(one[0], one[1], split[0], split[1])
 
 
-@pytest.mark.parametrize("streams", [0, 1], ids=["fused", "trace_streams"])
 @pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene"])
-def test_deferred_combine_across_async_calls(pt, name, streams):
+def test_deferred_combine_across_async_calls(pt, name):
     """Back-to-back hipptRenderFramesAsync calls: each megakernel batch's combine (running average
-    + tonemap) runs inside the next batch's launch (Ctx::deferred), from the other scratch buffer,
-    or (HIPPT_OPT_TRACE_STREAMS 1) batches trace on two streams into slots of their own while the
-    context's stream combines them in order; anything that reads or resets the image runs the
-    pending work first.  Every sequence below gives the oracle's progressive image bit for bit."""
+    + tonemap) runs inside the next batch's launch (Ctx::deferred), from the other scratch buffer;
+    anything that reads or resets the image runs the pending one first.  Every sequence below
+    gives the oracle's progressive image bit for bit."""
     sc = scenes.get_scene(name)
     w, h = 45, 26
     ora6 = po.MeshScene(sc, w, h).frames(0, 6, 8)
-    pt.setOption(hippt.OPT_TRACE_STREAMS, streams)
     pt.uploadMesh(sc)
     # fused off: every batch's combine its own launch
     pt.setOption(hippt.OPT_FUSE_COMBINE, 0)
