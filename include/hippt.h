@@ -231,11 +231,6 @@ enum {
                                        batch's launch on the same device (beside its paths) instead of as a
                                        launch of its own, whenever nothing reads the image in between (1), or
                                        never (0); -1 (default): automatic.  Same results either way */
-    , HIPPT_OPT_PRIMARY_LISTS = 28  /* megakernel, Lambertian triangle scenes, pinhole camera: each camera ray
-                                       tests the primitives listed for its pixel (those whose projection can
-                                       cover it, built on the host per camera and image size) instead of
-                                       traversing the BVH (1), or traverses (0); -1 (default): automatic.
-                                       Same results either way */
 };
 /* Output frame word formats (HIPPT_OPT_PIXEL_FORMAT).  Both map an accumulated colour c to
  * sqrt(clamp(c, 0, 1)) per channel.
@@ -247,7 +242,7 @@ enum {
 enum { HIPPT_PIXEL_ARGB = 0, HIPPT_PIXEL_RGBA8 = 1 };
 /* Read-only (hipptGetOption) facts of the last megakernel render: LDS bytes of the top of the tree,
  * persistent-grid blocks per CU. */
-enum { HIPPT_INFO_LDS_TOP_BYTES = 100, HIPPT_INFO_BLOCKS_PER_CU = 101, HIPPT_INFO_PRIMARY_CANDIDATES = 102 };
+enum { HIPPT_INFO_LDS_TOP_BYTES = 100, HIPPT_INFO_BLOCKS_PER_CU = 101 };
 bool hipptSetOption(int key, long long value);
 long long hipptGetOption(int key);
 /* BVH width (2 or 4) the last mesh render traversed (0 before any): what nodeVisits count. */
@@ -282,15 +277,6 @@ void hipptBvh4QCopy(const hipptBvh *bvh, uint32_t *nodes);
 /* Nodes of that 8-bit tree: Bvh4NodeCount, or 0 when the scene has none (boxes near +-FLT_MAX,
  * which no finite grid covers; the kernels then read the float nodes). */
 int hipptBvh4QNodeCount(const hipptBvh *bvh);
-
-/* Primary candidate lists (HIPPT_OPT_PRIMARY_LISTS) of numTris triangles (verts: 9 floats each, as
- * hipptSetMeshScene) for the pixels of rows y0, y0+stride, ... (rows of them) of a width x height
- * image seen by a pinhole camera: ids[offsets[p] .. offsets[p+1]) are the triangles whose FP32
- * ray test can pass for some camera ray through band pixel p = k*width + x (ascending).  offsets
- * (rows*width+1 words) is written when non-NULL, ids when idsCapacity covers the total.  Returns
- * the total, or -1 for a lens camera or bad arguments. */
-long long hipptPrimaryLists(const float *verts, int numTris, const hipptCamera *camera, int width, int height,
-                            int y0, int rows, int stride, uint32_t *offsets, uint32_t *ids, long long idsCapacity);
 
 #ifdef __cplusplus
 }

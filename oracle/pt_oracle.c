@@ -217,30 +217,6 @@ int po_closest_hit(const po_tri *tris, const int *orig_ids, int ntris, const flo
     return best_i;
 }
 
-void po_pixel_any_hits(const po_tri *tris, int ntris, const po_camera *cam, int width, int height, int x, int y,
-                       int n, int extra, uint32_t seed, float tmin, unsigned char *hit) {
-    const float invW = 1.0f / (float)(width > 1 ? width - 1 : 1);
-    const float invH = 1.0f / (float)(height > 1 ? height - 1 : 1);
-    uint32_t rng = po_hash32(seed ^ po_hash32((uint32_t)(x * 73856093) ^ (uint32_t)(y * 19349663)));
-    const int grid = n > 0 ? (n + 1) * (n + 1) : 0;
-    for (int r = 0; r < grid + extra; ++r) {
-        float a, b;
-        if (r < grid) {
-            a = (float)(r % (n + 1)) / (float)n;
-            b = (float)(r / (n + 1)) / (float)n;
-        } else {
-            a = po_rand01(&rng);
-            b = po_rand01(&rng);
-        }
-        const float s = ((float)x + a) * invW, t = ((float)y + b) * invH;
-        uint32_t st = 1u;
-        float o[3], d[3], tt;
-        po_camera_get_ray(cam, s, t, &st, o, d);
-        for (int k = 0; k < ntris; ++k)
-            if (!hit[k] && po_tri_hit(&tris[k], o, d, tmin, &tt)) hit[k] = 1;
-    }
-}
-
 /* Sphere::hit — RayTracer.h:289-314 in FP32 (plain ops). */
 int po_sphere_hit(const float c[3], float r, const float o[3], const float d[3], float tmin, float tmax,
                   float *t, float n[3], int *front) {

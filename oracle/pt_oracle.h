@@ -77,12 +77,6 @@ void po_camera_get_ray(const po_camera *cam, float s, float t, uint32_t *state, 
 /* Closest hit over a triangle list, brute force.  Returns index (into tris) or -1. */
 int po_closest_hit(const po_tri *tris, const int *orig_ids, int ntris, const float o[3], const float d[3],
                    float tmin, float *t_out);
-/* Test support for the primary candidate lists (hipptPrimaryLists): for pixel (x, y) of a width x
- * height image, the camera rays through footprint points (x + i/n, y + j/n), 0 <= i, j <= n, and
- * `extra` seeded random points, in the kernels' FP32 arithmetic (s = (x + a) * (1/(W-1))); sets
- * hit[k] = 1 for every triangle k that po_tri_hit reports hit (t >= tmin) by any of them. */
-void po_pixel_any_hits(const po_tri *tris, int ntris, const po_camera *cam, int width, int height, int x, int y,
-                       int n, int extra, uint32_t seed, float tmin, unsigned char *hit);
 
 /* ---- sphere4: the legacy CUDA kernel (CudaPathTracerKernel.cu:136-179) ---- */
 /* Renders one frame for rows [y0, y1) of a width x height image.

@@ -66,8 +66,6 @@ def lib() -> ctypes.CDLL:
     sig("po_random_in_unit_disk", None, pu32, pf)
     sig("po_camera_get_ray", None, ctypes.POINTER(PoCamera), f, f, pu32, pf, pf)
     sig("po_closest_hit", i, ctypes.POINTER(PoTri), pi, i, pf, pf, f, pf)
-    sig("po_pixel_any_hits", None, ctypes.POINTER(PoTri), i, ctypes.POINTER(PoCamera), i, i, i, i, i, i, u32, f,
-        ctypes.POINTER(ctypes.c_uint8))
     sig("po_sphere4_frames", None, i, i, i, i, i, i, i, pf, pu32, i)
     sig("po_scene_create", ctypes.c_void_p, pf, pi, i, pf, i, ctypes.POINTER(PoCamera), i)
     sig("po_scene_create2", ctypes.c_void_p, pf, pi, i, pf, pi, i, ctypes.c_void_p, i, ctypes.POINTER(PoCamera), i)
@@ -222,23 +220,6 @@ def closest_hit(scene, o, d, tmin=0.001):
     t = ctypes.c_float()
     idx = lib().po_closest_hit(tris, None, scene.num_tris, f3(o), f3(d), float(tmin), ctypes.byref(t))
     return idx, t.value
-
-
-def tri_array(verts) -> ctypes.Array:
-    """po_tri_setup of every triangle (verts (n, 9))."""
-    v = np.ascontiguousarray(verts, np.float32).reshape(-1, 9)
-    tris = (PoTri * v.shape[0])()
-    for i in range(v.shape[0]):
-        lib().po_tri_setup(v[i].ctypes.data_as(ctypes.POINTER(ctypes.c_float)), ctypes.byref(tris[i]))
-    return tris
-
-
-def pixel_any_hits(tris, cam: PoCamera, width, height, x, y, n=4, extra=0, seed=1, tmin=0.001) -> np.ndarray:
-    """Indices of the triangles some camera ray through pixel (x, y) hits (po_pixel_any_hits)."""
-    hit = np.zeros(len(tris), np.uint8)
-    lib().po_pixel_any_hits(tris, len(tris), ctypes.byref(cam), width, height, x, y, n, extra, seed, float(tmin),
-                            hit.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)))
-    return np.flatnonzero(hit)
 
 
 def argb_to_rgb(img: np.ndarray) -> np.ndarray:

@@ -9,7 +9,6 @@
 //   * triangle-mesh scenes with a host-built SAH BVH in addition to the reference's
 //     built-in 4-sphere scene.
 #include "../../include/hippt.h"
-#include "primary_lists.h"
 
 #include <hip/hip_runtime.h>
 
@@ -82,13 +81,6 @@ struct Ctx {
     float4 *nodes4q = nullptr; // the 4-wide BVH with 8-bit child boxes
     float4 *nodes4h = nullptr; // hybrid layout (float top + 8-bit nodes) for hybridTop top nodes
     int hybridTop = -1;
-    // primary candidate lists of this context's rows (HIPPT_OPT_PRIMARY_LISTS), built per key
-    uint32_t *primOff = nullptr, *primIds = nullptr;
-    long long primCount = -1;  // candidates listed (-1: none built; 0: lists off for this key)
-    struct PrimKey {
-        int version = -1, width = 0, height = 0, y0 = 0, rows = 0, stride = 0;
-        CameraF cam{};
-    } primKey;
     int *spill = nullptr;      // 4-wide traversal: per-lane stack spill area
     size_t spillBytes = 0;
     // wavefront path-state pool (allocated on first use)
@@ -165,8 +157,6 @@ struct State {
     int pixelFormat = HIPPT_PIXEL_ARGB;  // output frame words (HIPPT_OPT_PIXEL_FORMAT)
     int cameraPool = -1;  // megakernel camera-ray pool (HIPPT_OPT_CAMERA_POOL; -1: automatic)
     int fuseCombine = -1;  // combine inside the next megakernel launch (HIPPT_OPT_FUSE_COMBINE)
-    int primaryLists = -1;  // per-pixel primary candidate lists (HIPPT_OPT_PRIMARY_LISTS; -1: automatic)
-    long long activePrimCount = -1;  // candidates listed for the last mesh render's context (-1: lists off)
     std::vector<std::pair<int, uint32_t *>> rngTables;  // per device, built on first use
     unsigned activeTopBytes = 0;  // of the last mesh render (hipptGetOption HIPPT_INFO_*)
     int activeBlocksPerCu = 0;
@@ -187,11 +177,6 @@ State &S() {
     static State s;
     return s;
 }
-
-// A triangle's device record (MeshParams::tris, 3 float4: (v0, e1.x) (e1.yz, e2.xy) (e2.z, id,
-// tag 0, -)) and unit normal: po_tri_setup (oracle) restated, e1 = v1-v0, e2 = v2-v0, n =
-// cross/len, a degenerate triangle (len 0) with zero edges.
-void tri_record(const float *v, int id, float4 *rec, float n[3]);
 
 bool fail(const char **errorMessage, const std::string &msg) {
     State &s = S();
@@ -218,25 +203,6 @@ inline float as_float(int v) {
     float f;
     std::memcpy(&f, &v, 4);
     return f;
-}
-
-void tri_record(const float *v, int id, float4 *rec, float n[3]) {
-    float e1[3] = {v[3] - v[0], v[4] - v[1], v[5] - v[2]};
-    float e2[3] = {v[6] - v[0], v[7] - v[1], v[8] - v[2]};
-    float cr[3];
-    fcross(e1, e2, cr);
-    const float len = std::sqrt(fdot(cr, cr));
-    if (!(len > 0.0f)) {
-        e1[0] = e1[1] = e1[2] = 0.0f;
-        e2[0] = e2[1] = e2[2] = 0.0f;
-        n[0] = n[1] = n[2] = 0.0f;
-    } else {
-        const float inv = 1.0f / len;
-        for (int a = 0; a < 3; ++a) n[a] = cr[a] * inv;
-    }
-    rec[0] = float4{v[0], v[1], v[2], e1[0]};
-    rec[1] = float4{e1[1], e1[2], e2[0], e2[1]};
-    rec[2] = float4{e2[2], as_float(id), 0.0f, 0.0f};
 }
 
 // RayTracer.h Camera::Camera (:545-561), FP64, stored FP32.
@@ -289,11 +255,6 @@ void free_scene_buffers(Ctx &c) {
     (void)hipFree(c.nodes4h);
     c.nodes = c.tris = c.shade = c.mats = c.nodes4 = c.nodes4q = c.nodes4h = nullptr;
     c.hybridTop = -1;
-    (void)hipFree(c.primOff);
-    (void)hipFree(c.primIds);
-    c.primOff = c.primIds = nullptr;
-    c.primCount = -1;
-    c.primKey = Ctx::PrimKey{};
     c.sceneVersion = -1;
 }
 
@@ -423,48 +384,6 @@ unsigned packed_ref_bits(int numNodes, int numPrims) {
 
 // The hybrid node layout (bvh_builder.h hybrid_bvh4) for `top` top-of-tree nodes: built on the
 // host once per (scene, top) and uploaded to the context's device.
-// The primary candidate lists of a context's rows for this scene, camera and image (built on the
-// host, primary_lists.cpp, and kept until one of them changes).  `ok` = lists usable: false for
-// scenes with spheres, lens cameras, or lists averaging more than kPrimMaxMean candidates per pixel
-// (the traversal is cheaper then).
-constexpr long long kPrimMaxMean = 8;
-bool ensure_primary(Ctx &c, const CameraF &cam, bool &ok, const char **err) {
-    State &s = S();
-    Ctx::PrimKey key;
-    key.version = s.scene.version;
-    key.width = s.width;
-    key.height = s.height;
-    key.y0 = c.y0;
-    key.rows = c.rows;
-    key.stride = c.stride;
-    key.cam = cam;
-    if (c.primCount >= 0 && std::memcmp(&key, &c.primKey, sizeof key) == 0) {
-        ok = c.primCount > 0;
-        return true;
-    }
-    std::vector<uint32_t> off, ids;
-    ok = hippt::build_primary_lists(reinterpret_cast<const float *>(s.scene.tris.data()), s.scene.numTris, cam,
-                                    s.width, s.height, c.y0, c.rows, c.stride, off, ids);
-    const long long pixels = (long long)c.rows * s.width;
-    if (ok && (long long)ids.size() > kPrimMaxMean * std::max(1LL, pixels)) ok = false;
-    HIP_TRY(hipSetDevice(c.device));
-    HIP_TRY(hipStreamSynchronize(c.stream));  // launches in flight read the old lists
-    (void)hipFree(c.primOff);
-    (void)hipFree(c.primIds);
-    c.primOff = c.primIds = nullptr;
-    c.primKey = key;
-    c.primCount = 0;
-    if (ok) {
-        HIP_TRY(hipMalloc(&c.primOff, off.size() * sizeof(uint32_t)));
-        HIP_TRY(hipMalloc(&c.primIds, std::max<size_t>(1, ids.size()) * sizeof(uint32_t)));
-        HIP_TRY(hipMemcpy(c.primOff, off.data(), off.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        if (!ids.empty())
-            HIP_TRY(hipMemcpy(c.primIds, ids.data(), ids.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
-        c.primCount = std::max<long long>(1, (long long)ids.size());
-    }
-    return true;
-}
-
 bool ensure_hybrid(Ctx &c, int top, const char **err) {
     State &s = S();
     SceneHost &sc = s.scene;
@@ -841,16 +760,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 if (hybrid) quant = false;  // (pool: off, as for 8-bit nodes)
                 const bool pinhole = cam.lens_radius == 0.0f && cam.origin[0] != 0.0f && cam.origin[1] != 0.0f &&
                                      cam.origin[2] != 0.0f;
-                // Primary candidate lists (megakernel, Lambertian triangles, pinhole camera): a camera
-                // ray tests its pixel's list instead of traversing; computed beside the ray in the pool.
-                bool primLists = false;
-                if (s.pathMode == 0 && !s.scene.full && s.primaryLists != 0 && cam.lens_radius == 0.0f &&
-                    maxDepth > 0 && !ensure_primary(c, cam, primLists, err))
-                    return false;
-                s.activePrimCount = primLists ? c.primCount : -1;
-                const int poolWords = pool ? (pinhole ? hippt::kPoolWordsPinhole : hippt::kPoolWordsFull) +
-                                                 (primLists ? hippt::kPoolWordsHit : 0)
-                                           : 0;
+                const int poolWords = pool ? (pinhole ? hippt::kPoolWordsPinhole : hippt::kPoolWordsFull) : 0;
                 unsigned topBytes = 0;
                 if (topTree && s.ldsTopNodes != 0) {
                     const size_t nodeBytes = quant ? 64 : 128;  // hybrid: a float top
@@ -945,8 +855,6 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.refBits = ldsScene && wide ? packed_ref_bits(numNodes, numTris) : 0u;
                         p.rngTable = nullptr;
                         p.poolWords = poolWords;
-                        p.primOff = primLists ? c.primOff : nullptr;
-                        p.primIds = primLists ? c.primIds : nullptr;
                         p.poolOffset = unsigned(hippt::mesh_lds_bytes(stackDepth, ldsScene ? numNodes : 0,
                                                                       ldsScene ? numTris : 0, wide, topBytes,
                                                                       ldsScene ? numMats : 0));
@@ -1178,8 +1086,24 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
                 float4{q[0], q[1], q[2], as_float(sphereMaterial[id - numTris] | hippt::kShadeSphere)};
             continue;
         }
-        float n[3];
-        tri_record(verts + 9 * size_t(id), id, &sc.tris[3 * size_t(k)], n);
+        const float *v = verts + 9 * size_t(id);
+        // po_tri_setup (oracle) restated: e1 = v1-v0, e2 = v2-v0, n = cross/len
+        float e1[3] = {v[3] - v[0], v[4] - v[1], v[5] - v[2]};
+        float e2[3] = {v[6] - v[0], v[7] - v[1], v[8] - v[2]};
+        float cr[3], n[3];
+        fcross(e1, e2, cr);
+        const float len = std::sqrt(fdot(cr, cr));
+        if (!(len > 0.0f)) {
+            e1[0] = e1[1] = e1[2] = 0.0f;
+            e2[0] = e2[1] = e2[2] = 0.0f;
+            n[0] = n[1] = n[2] = 0.0f;
+        } else {
+            const float inv = 1.0f / len;
+            for (int a = 0; a < 3; ++a) n[a] = cr[a] * inv;
+        }
+        sc.tris[3 * size_t(k)] = float4{v[0], v[1], v[2], e1[0]};
+        sc.tris[3 * size_t(k) + 1] = float4{e1[1], e1[2], e2[0], e2[1]};
+        sc.tris[3 * size_t(k) + 2] = float4{e2[2], as_float(id), 0.0f, 0.0f};
         sc.shade[size_t(k)] = float4{n[0], n[1], n[2], as_float(triMaterial[id])};
     }
     sc.mats.assign(size_t(numMaterials) * 2, float4{});
@@ -1557,10 +1481,6 @@ extern "C" bool hipptSetOption(int key, long long value) {
         if (value < -1 || value > 1) return false;
         s.fuseCombine = int(value);
         return true;
-    case HIPPT_OPT_PRIMARY_LISTS:
-        if (value < -1 || value > 1) return false;
-        s.primaryLists = int(value);
-        return true;
     default: return false;
     }
 }
@@ -1600,8 +1520,6 @@ extern "C" long long hipptGetOption(int key) {
     case HIPPT_OPT_PIXEL_FORMAT: return s.pixelFormat;
     case HIPPT_OPT_CAMERA_POOL: return s.cameraPool;
     case HIPPT_OPT_FUSE_COMBINE: return s.fuseCombine;
-    case HIPPT_OPT_PRIMARY_LISTS: return s.primaryLists;
-    case HIPPT_INFO_PRIMARY_CANDIDATES: return s.activePrimCount;
     case HIPPT_INFO_LDS_TOP_BYTES: return s.activeTopBytes;
     case HIPPT_INFO_BLOCKS_PER_CU: return s.activeBlocksPerCu;
     default: return -1;
@@ -1652,23 +1570,4 @@ extern "C" int hipptBvh4QNodeCount(const hipptBvh *b) {
 }
 extern "C" void hipptBvh4QCopy(const hipptBvh *b, uint32_t *nodes) {
     if (b && nodes) std::memcpy(nodes, b->bvh4q.data(), b->bvh4q.size() * sizeof(uint32_t));
-}
-
-extern "C" long long hipptPrimaryLists(const float *verts, int numTris, const hipptCamera *camera, int width,
-                                       int height, int y0, int rows, int stride, uint32_t *offsets, uint32_t *ids,
-                                       long long idsCapacity) {
-    if ((!verts && numTris > 0) || numTris < 0 || !camera || rows < 0) return -1;
-    std::vector<float4> recs(size_t(numTris) * 3);
-    float n[3];
-    for (int k = 0; k < numTris; ++k) tri_record(verts + 9 * size_t(k), k, &recs[3 * size_t(k)], n);
-    CameraF cam;
-    static_assert(sizeof(CameraF) == sizeof(hipptCamera), "hipptCamera layout");
-    std::memcpy(&cam, camera, sizeof cam);
-    std::vector<uint32_t> off, list;
-    if (!hippt::build_primary_lists(reinterpret_cast<const float *>(recs.data()), numTris, cam, width, height, y0,
-                                    rows, stride, off, list))
-        return -1;
-    if (offsets) std::memcpy(offsets, off.data(), off.size() * sizeof(uint32_t));
-    if (ids && idsCapacity >= (long long)list.size()) std::memcpy(ids, list.data(), list.size() * sizeof(uint32_t));
-    return (long long)list.size();
 }

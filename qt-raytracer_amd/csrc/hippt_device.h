@@ -82,10 +82,6 @@ struct MeshParams {
     // LDS-resident 4-wide trees: low bits of a packed child key that carry the child's code
     // (trace::child_key_p; hippt_api.cpp packed_ref_bits)
     unsigned refBits;
-    // pinhole cameras, Lambertian triangle scenes (null otherwise): per band pixel p, the
-    // primitive slots primIds[primOff[p] .. primOff[p+1]) that can be the closest hit of the
-    // pixel's camera rays (primary_lists.h); the kernel tests those instead of traversing
-    const unsigned *primOff, *primIds;
     // random_in_unit_sphere memoized (null: the rejection loop): entry 2^32-word table, see
     // launch_rng_table
     const uint32_t *rngTable;
@@ -134,8 +130,6 @@ size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide, unsi
 // camera-ray pool words per ray: item, rng, direction (+ origin unless every ray starts at the
 // camera origin)
 constexpr int kPoolWordsPinhole = 5, kPoolWordsFull = 8;
-// + the primary hit (t, primitive slot) when the primary lists are on (MeshParams::primOff)
-constexpr int kPoolWordsHit = 2;
 // LDS bytes per block that keep the persistent grid's resident blocks within a CU's LDS
 size_t mesh_lds_block_budget();
 size_t mesh_lds_scene_limit();

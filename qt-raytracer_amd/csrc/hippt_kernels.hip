@@ -251,28 +251,16 @@ __device__ __forceinline__ bool combine_chunk(const MeshParams &P) {
 // more entries than it holds (those lanes take the rest of the old pool first, then the new one).
 // Items are claimed from the work queue in the same order as without the pool and every claimed
 // item is traced, so the results are the same.
-constexpr int kPrimTraverse = -2;  // pool hit slot: the ray's list was too long, traverse
-
-// Pool formats: kPoolWordsPinhole or kPoolWordsFull words per entry, + kPoolWordsHit when the
-// primary lists are on (the entry then carries its ray's closest hit, computed with the ray).
-__device__ __forceinline__ bool pool_has_origin(int words) {
-    return words == kPoolWordsFull || words == kPoolWordsFull + kPoolWordsHit;
-}
-__device__ __forceinline__ bool pool_has_hit(int words) {
-    return words == kPoolWordsPinhole + kPoolWordsHit || words == kPoolWordsFull + kPoolWordsHit;
-}
-
 template <bool POOL>
 __device__ __forceinline__ void pool_take(const MeshParams &P, const float *pool, unsigned k, unsigned &item, Ray &r,
-                                          uint32_t &rng, Trav &T, bool &prim) {
+                                          uint32_t &rng) {
     item = __float_as_uint(pool[k]);
     if (item == kNone) return;
     rng = __float_as_uint(pool[64 + k]);
     r.dx = pool[128 + k];
     r.dy = pool[192 + k];
     r.dz = pool[256 + k];
-    const bool hasO = pool_has_origin(P.poolWords);
-    if (hasO) {
+    if (P.poolWords == kPoolWordsFull) {
         r.ox = pool[320 + k];
         r.oy = pool[384 + k];
         r.oz = pool[448 + k];
@@ -280,19 +268,6 @@ __device__ __forceinline__ void pool_take(const MeshParams &P, const float *pool
         r.ox = P.cam.origin[0];
         r.oy = P.cam.origin[1];
         r.oz = P.cam.origin[2];
-    }
-    if (pool_has_hit(P.poolWords)) {
-        const unsigned h = (hasO ? kPoolWordsFull : kPoolWordsPinhole) * 64u + k;
-        const int hitI = __float_as_int(pool[h + 64]);
-        if (hitI != kPrimTraverse) {
-            T.bestT = pool[h];
-            T.bestI = hitI;
-            T.cur = kDone;
-            T.leaf = 0;
-            T.sp = 0;
-            T.ovf = 0;
-            prim = true;
-        }
     }
 }
 
@@ -319,8 +294,6 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     // Trees in global memory (4-wide): the top of the tree (P.topBytes of the node array) at LDS
     // address 0, then the stack.
     constexpr bool TOP = WIDE && !LDS_SCENE;
-    // primary lists (MeshParams::primOff): the Lambertian-triangle kernels
-    constexpr bool PRIM = !FULL;
     // packed child keys: the Lambertian kernel over LDS-resident 4-wide trees (Cornell +0.8%; the
     // general kernel lost 4.3% with them, cornell_mixed, round 3 A/B)
     constexpr bool PACKED = WIDE && LDS_SCENE && !FULL && bool(HIPPT_PACKED_KEYS);
@@ -389,7 +362,6 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     T.bestO = 0x7fffffff;
     float tr = 1, tg = 1, tb = 1;
     bool need = true, fresh = false;
-    bool prim = false;  // the fresh camera ray's closest hit is already known (primary lists)
     constexpr unsigned CAP = FULL ? 0u : unsigned(HIPPT_REJECT_CAP);
     unsigned pend = 0;  // tries so far of a pending unit-sphere draw (CAP), 0 = none
     // per-lane counts fit 32 bits (a lane traces a few thousand segments per launch); widened
@@ -417,7 +389,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                 const bool took = need;
                 if (need && rank < avail) {
                     need = false;
-                    pool_take<POOL>(P, pool, poolNext + rank, item, r, rng, T, prim);
+                    pool_take<POOL>(P, pool, poolNext + rank, item, r, rng);
                 }
                 if (n > avail) {
                     // the camera rays of the wave's next 64 items, every lane at once
@@ -428,21 +400,9 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
 #endif
                     Ray c{};
                     uint32_t crng = 0;
-                    unsigned pix = 0;
-                    float hitT = 0.0f;
-                    int hitI = -1;
                     if (it != kNone) {
                         prof<STATS>(pc, 1);
-                        camera_sample(P, it, c, crng, &pix);
-                        if (PRIM && P.primOff) {  // the closest hit of the new camera ray, all lanes at once
-                            Trav H;
-                            if (primary_hit<STATS>(P, pix, c, tris, H, ntest, pc)) {
-                                hitT = H.bestT;
-                                hitI = H.bestI;
-                            } else {
-                                hitI = kPrimTraverse;
-                            }
-                        }
+                        camera_sample(P, it, c, crng);
                     }
                     const unsigned k = __lane_id();
                     pool[k] = __uint_as_float(it);
@@ -450,21 +410,15 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                     pool[128 + k] = c.dx;
                     pool[192 + k] = c.dy;
                     pool[256 + k] = c.dz;
-                    const bool hasO = pool_has_origin(P.poolWords);
-                    if (hasO) {
+                    if (P.poolWords == kPoolWordsFull) {
                         pool[320 + k] = c.ox;
                         pool[384 + k] = c.oy;
                         pool[448 + k] = c.oz;
                     }
-                    if (PRIM && pool_has_hit(P.poolWords)) {
-                        const unsigned h = (hasO ? kPoolWordsFull : kPoolWordsPinhole) * 64u + k;
-                        pool[h] = hitT;
-                        pool[h + 64] = __int_as_float(hitI);
-                    }
                     poolNext = n - avail;
                     if (need) {
                         need = false;
-                        pool_take<POOL>(P, pool, rank - avail, item, r, rng, T, prim);
+                        pool_take<POOL>(P, pool, rank - avail, item, r, rng);
                     }
                 } else {
                     poolNext += n;
@@ -486,9 +440,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                 item = it;
                 if (it != kNone) {
                     prof<STATS>(pc, 1);
-                    unsigned pix = 0;
-                    camera_sample(P, it, r, rng, &pix);
-                    if (PRIM && P.primOff) prim = primary_hit<STATS>(P, pix, r, tris, T, ntest, pc);
+                    camera_sample(P, it, r, rng);
                     tr = tg = tb = 1.0f;
                     depth = 0;
                     fresh = true;
@@ -500,13 +452,9 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         if (fresh) {
             fresh = false;
             prepare(r);
-            if (PRIM && prim)
-                prim = false;  // traversal already done (primary_hit)
-            else
-                begin(T);
+            begin(T);
         }
-        // (a lane whose camera ray's hit came from its primary list is live but not busy)
-        if (!__any(PRIM ? item != kNone : (busy(T) || pend != 0u))) break;
+        if (!__any(busy(T) || pend != 0u)) break;
 
 
         // ---- traversal: while-while over the BVH; leave once few lanes remain -------------
@@ -712,10 +660,8 @@ hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hip
     if (p.wide == kWideHybrid && !p.topBytes) return hipErrorInvalidValue;  // hybrid trees start in LDS
     if (lds && p.wide == kWideFloat && (p.refBits < 8 || p.refBits > 20)) return hipErrorInvalidValue;
     const bool pool = p.poolWords != 0;
-    const int baseWords = p.primOff ? p.poolWords - kPoolWordsHit : p.poolWords;
-    if (pool && (p.wide != kWideFloat || (baseWords != kPoolWordsPinhole && baseWords != kPoolWordsFull)))
+    if (pool && (p.wide != kWideFloat || (p.poolWords != kPoolWordsPinhole && p.poolWords != kPoolWordsFull)))
         return hipErrorInvalidValue;
-    if (p.primOff && (p.full || p.cam.lens_radius != 0.0f)) return hipErrorInvalidValue;
     const size_t bytes = mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0, p.wide != 0, p.topBytes,
                                         lds ? p.numMats : 0, p.poolWords);
     if (pool && p.poolOffset != bytes - size_t(p.poolWords) * kMeshBlock * sizeof(float)) return hipErrorInvalidValue;

@@ -256,11 +256,9 @@ __device__ __forceinline__ void prepare(Ray &r) {
 
 // Camera sample for work item `it`: RenderWorker::render u/v (RayTracerFboItem.cpp:109-110) and
 // Camera::get_ray (RayTracer.h:563-567, disk draw always consumed).
-__device__ __forceinline__ void camera_sample(const MeshParams &P, unsigned it, Ray &r, uint32_t &rng,
-                                              unsigned *pixel = nullptr) {
+__device__ __forceinline__ void camera_sample(const MeshParams &P, unsigned it, Ray &r, uint32_t &rng) {
     unsigned fl, p, yb, x;
     divmod(it, P.bandPixels, P.rcpBandPixels, fl, p);
-    if (pixel) *pixel = p;
     divmod(p, unsigned(P.width), P.rcpWidth, yb, x);
     const unsigned y = unsigned(P.y0) + yb * unsigned(P.rowStride);
     rng = pixel_seed(x, y, unsigned(P.width), unsigned(P.firstFrame) + fl);
@@ -583,29 +581,6 @@ __device__ __forceinline__ void test_prim(Trav &T, const Ray &r, const float4 *t
                                           unsigned *pc) {
     const float4 *tp = tris + 3 * i;
     test_prim_data<STATS, FULL>(T, r, tp[0], tp[1], tp[2], i, ntest, pc);
-}
-
-// The camera ray of band pixel p (pinhole camera): its closest hit among the pixel's candidate
-// primitives (MeshParams::primOff/primIds; primary_lists.cpp), which hold every primitive whose
-// FP32 test can pass for a ray through the pixel, tested in the same arithmetic: the result
-// (argmin (t, primitive id)) is the traversal's.  Leaves T finished (nothing left to traverse) and
-// returns true, or returns false for a list longer than kPrimListCap (the blob's poles, where many
-// degenerate triangles' strips cross): that ray traverses the tree instead.
-constexpr unsigned kPrimListCap = 32;
-template <bool STATS>
-__device__ __forceinline__ bool primary_hit(const MeshParams &P, unsigned p, const Ray &r, const float4 *tris, Trav &T,
-                                            unsigned long long &ntest, unsigned *pc) {
-    const unsigned b = P.primOff[p], e = P.primOff[p + 1];
-    if (e - b > kPrimListCap) return false;
-    T.bestT = INFINITY;
-    T.bestI = -1;
-    T.bestO = 0x7fffffff;
-    for (unsigned k = b; k < e; ++k) test_prim<STATS, false>(T, r, tris, int(P.primIds[k]), ntest, pc);
-    T.cur = kDone;
-    T.leaf = 0;
-    T.sp = 0;
-    T.ovf = 0;
-    return true;
 }
 
 // One leaf-loop iteration for this lane: the primitives of leaf T.leaf, then the next leaf if it

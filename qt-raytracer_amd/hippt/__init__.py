@@ -51,13 +51,11 @@ OPT_BVH_LEAF4 = 23
 OPT_RNG_TABLE = 24
 OPT_CAMERA_POOL = 26
 OPT_FUSE_COMBINE = 27
-OPT_PRIMARY_LISTS = 28
 OPT_PIXEL_FORMAT = 25
 PIXEL_ARGB = 0
 PIXEL_RGBA8 = 1
 INFO_LDS_TOP_BYTES = 100
 INFO_BLOCKS_PER_CU = 101
-INFO_PRIMARY_CANDIDATES = 102
 
 # Every symbol include/hippt.h declares (checked by tests/test_abi_cpu.py).
 EXPORTS = (
@@ -72,7 +70,7 @@ EXPORTS = (
     "hipptGetOption",
     "hipptLastError", "hipptBvhBuild", "hipptBvhNodeCount", "hipptBvhDepth", "hipptBvhCopy", "hipptBvhFree",
     "hipptBvh4NodeCount", "hipptBvh4Depth", "hipptBvh4StackBound", "hipptBvh4Copy", "hipptBvh4QCopy", "hipptBvh4QNodeCount",
-    "hipptActiveBvhWidth", "hipptPrimaryLists",
+    "hipptActiveBvhWidth",
 )
 
 
@@ -183,8 +181,6 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     sig("hipptBvh4Copy", None, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32))
     sig("hipptBvh4QCopy", None, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32))
     sig("hipptBvh4QNodeCount", c_int, ctypes.c_void_p)
-    sig("hipptPrimaryLists", ctypes.c_longlong, p_float, c_int, ctypes.POINTER(Camera), c_int, c_int, c_int, c_int,
-        c_int, ctypes.POINTER(ctypes.c_uint32), ctypes.POINTER(ctypes.c_uint32), ctypes.c_longlong)
     _lib = lib
     return lib
 
@@ -224,23 +220,6 @@ def build_camera(lookfrom, lookat, vup, vfov, aspect, aperture, focus) -> Camera
     lib.hipptBuildCamera(_d3(lookfrom), _d3(lookat), _d3(vup), float(vfov), float(aspect), float(aperture),
                          float(focus), ctypes.byref(cam))
     return cam
-
-
-def primary_lists(verts: np.ndarray, cam: Camera, width: int, height: int, y0: int = 0, rows: Optional[int] = None,
-                  stride: int = 1):
-    """hipptPrimaryLists: (offsets (rows*width+1,) uint32, ids uint32) of the band's pixels, or None
-    when the camera has a lens."""
-    lib = load_library()
-    v = np.ascontiguousarray(verts, dtype=np.float32).reshape(-1, 9)
-    rows = height if rows is None else rows
-    off = np.zeros(rows * width + 1, np.uint32)
-    args = (_ptr(v, ctypes.c_float), int(v.shape[0]), ctypes.byref(cam), width, height, y0, rows, stride)
-    n = lib.hipptPrimaryLists(*args, _ptr(off, ctypes.c_uint32), None, 0)
-    if n < 0:
-        return None
-    ids = np.zeros(max(1, n), np.uint32)
-    assert lib.hipptPrimaryLists(*args, None, _ptr(ids, ctypes.c_uint32), n) == n
-    return off, ids[:n]
 
 
 class Bvh:

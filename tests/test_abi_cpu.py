@@ -88,7 +88,6 @@ def test_options_validate():
     (hippt.OPT_RNG_TABLE, (0, 1), (-1, 2), 0),
     (hippt.OPT_CAMERA_POOL, (-1, 0, 1), (-2, 2), -1),
     (hippt.OPT_FUSE_COMBINE, (-1, 0, 1), (-2, 2), -1),
-    (hippt.OPT_PRIMARY_LISTS, (-1, 0, 1), (-2, 2), -1),
     (hippt.OPT_STACK_CAP, (0, 4, 30), (3, 31), 0),
     (hippt.OPT_BVH_QUANT, (-1, 0, 1, 2), (-2, 3), -1),
 ])
@@ -113,7 +112,6 @@ def test_info_keys_before_any_render():
     lib = hippt.load_library()
     assert lib.hipptGetOption(hippt.INFO_LDS_TOP_BYTES) >= 0
     assert lib.hipptGetOption(hippt.INFO_BLOCKS_PER_CU) >= 0
-    assert lib.hipptGetOption(hippt.INFO_PRIMARY_CANDIDATES) >= -1
     assert not lib.hipptSetOption(hippt.INFO_LDS_TOP_BYTES, 1)
 
 

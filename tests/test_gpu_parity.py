@@ -30,7 +30,7 @@ def pt():
                  (hippt.OPT_STACK_CAP, 0), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_LDS_TOP_NODES, -1),
                  (hippt.OPT_RNG_TABLE, 0), (hippt.OPT_BVH_COLLAPSE, -1), (hippt.OPT_BVH_NODE_COST, 200),
                  (hippt.OPT_BVH_LEAF4, 4), (hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_ARGB),
-                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1), (hippt.OPT_PRIMARY_LISTS, -1)):
+                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1)):
         t.setOption(k, v)
     t.resetStats()
     yield t
@@ -410,68 +410,6 @@ def test_camera_pool_does_not_change_results(pt, name, variant):
         st = pt.stats()
         assert st["segments"] == ora[2] and st["pixelSamples"] == ora[3]
         pt.resetStats()
-
-
-@pytest.mark.parametrize("name,variant,pool", [
-    ("cornell34", "pinhole", -1),      # LDS scene, camera pool: hits computed into the pool
-    ("cornell34", "pinhole", 0),       # LDS scene, rays generated one by one
-    ("cornell34", "zero_origin", 1),   # pool entries carry the origin (10 words)
-    ("blob70k", "pinhole", -1),        # tree in global memory; 3% of the lists over the cap traverse
-    ("blob70k", "pinhole", 1),
-])
-def test_primary_lists_do_not_change_results(pt, name, variant, pool):
-    """HIPPT_OPT_PRIMARY_LISTS: camera rays test their pixel's candidate list instead of traversing
-    the BVH; the image is the oracle's bit for bit with the lists on and off, at sizes that are not
-    multiples of the pool or the wave, and for interleaved rows (each context its own lists)."""
-    sc = scenes.get_scene(name)
-    if variant == "zero_origin":
-        sc.lookfrom = (0.0, 278.0, -800.0)
-    w, h, frames = (53, 29, 3) if name == "cornell34" else (480, 270, 2)
-    ora = po.MeshScene(sc, w, h).frames(0, frames, 8)
-    pt.uploadMesh(sc)
-    pt.setOption(hippt.OPT_CAMERA_POOL, pool)
-    lib = hippt.load_library()
-    for lists in (1, 0, -1):
-        pt.setOption(hippt.OPT_PRIMARY_LISTS, lists)
-        assert pt.initialize(w, h), pt.lastError()
-        assert pt.renderFrames(frames, 8), pt.lastError()
-        got = pt.readback()
-        _assert_same(got[0], got[1], ora[0], ora[1])
-        st = pt.stats()
-        assert st["segments"] == ora[2] and st["pixelSamples"] == ora[3]
-        pt.resetStats()
-        cand = lib.hipptGetOption(hippt.INFO_PRIMARY_CANDIDATES)
-        assert (cand > 0) if lists == 1 else (cand == -1 if lists == 0 else True), (lists, cand)
-    pt.setOption(hippt.OPT_PRIMARY_LISTS, 1)
-    for phase, stride in ((1, 3), (0, 2)):
-        pt.setRowInterleave(phase, stride)
-        assert pt.initialize(w, h)
-        assert pt.renderFrames(frames, 8)
-        got = pt.readback()
-        rows = np.arange(phase, h, stride)
-        _assert_same(got[0][rows], got[1][rows], ora[0][rows], ora[1][rows])
-    pt.setRowRange(0, 0)
-
-
-def test_primary_lists_follow_the_camera(pt):
-    """The lists are rebuilt when the camera moves (hipptSetCamera) and when a lens camera turns
-    them off; every image is the oracle's for that camera."""
-    sc = scenes.get_scene("cornell34")
-    w, h = 45, 31
-    pt.uploadMesh(sc)
-    pt.setOption(hippt.OPT_PRIMARY_LISTS, 1)
-    lib = hippt.load_library()
-    for lookfrom, aperture in (((278.0, 278.0, -800.0), 0.0), ((150.0, 300.0, -600.0), 0.0),
-                               ((150.0, 300.0, -600.0), 20.0), ((400.0, 200.0, -700.0), 0.0)):
-        cam = hippt.build_camera(lookfrom, (278.0, 278.0, 0.0), (0.0, 1.0, 0.0), 40.0, w / h, aperture, 800.0)
-        assert lib.hipptSetCamera(cam, None)
-        assert pt.initialize(w, h)
-        assert pt.renderFrames(2, 8)
-        got = pt.readback()
-        ora = po.MeshScene(sc, w, h, cam=po.PoCamera.from_buffer_copy(bytes(cam))).frames(0, 2, 8)
-        _assert_same(got[0], got[1], ora[0], ora[1])
-        cand = lib.hipptGetOption(hippt.INFO_PRIMARY_CANDIDATES)
-        assert (cand == -1) if aperture else (cand > 0)
 
 
 @pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene"])
