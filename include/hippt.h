@@ -231,10 +231,6 @@ enum {
                                        batch's launch on the same device (beside its paths) instead of as a
                                        launch of its own, whenever nothing reads the image in between (1), or
                                        never (0); -1 (default): automatic.  Same results either way */
-    , HIPPT_OPT_SHADE_SORT = 28     /* wavefront, scenes with spheres or Metal/Dielectric materials: each shade
-                                       block orders its queue entries by material kind (misses, Lambertian,
-                                       Metal, Dielectric) before shading (1), or not (0); -1 (default):
-                                       automatic.  Same results either way */
 };
 /* Output frame word formats (HIPPT_OPT_PIXEL_FORMAT).  Both map an accumulated colour c to
  * sqrt(clamp(c, 0, 1)) per channel.

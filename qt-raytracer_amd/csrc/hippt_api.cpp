@@ -157,7 +157,6 @@ struct State {
     int pixelFormat = HIPPT_PIXEL_ARGB;  // output frame words (HIPPT_OPT_PIXEL_FORMAT)
     int cameraPool = -1;  // megakernel camera-ray pool (HIPPT_OPT_CAMERA_POOL; -1: automatic)
     int fuseCombine = -1;  // combine inside the next megakernel launch (HIPPT_OPT_FUSE_COMBINE)
-    int shadeSort = -1;    // wavefront shade blocks ordered by material kind (HIPPT_OPT_SHADE_SORT)
     std::vector<std::pair<int, uint32_t *>> rngTables;  // per device, built on first use
     unsigned activeTopBytes = 0;  // of the last mesh render (hipptGetOption HIPPT_INFO_*)
     int activeBlocksPerCu = 0;
@@ -602,12 +601,11 @@ bool run_wavefront(Ctx &c, hippt::MeshParams p, bool cnt, bool spills, int spill
     // (a polled loop alone runs up to 2*kPollEvery - 1 empty iterations past the end; the poll
     // still ends a deep maxDepth early once every path has ended).
     const bool allInFlight = slots >= p.totalItems;
-    const bool shadeSort = p.full && s.shadeSort == 1;
     for (long long it = 0;; ++it) {
         if (allInFlight && it == p.maxDepth) break;
         if (it > maxIter) return fail(err, "wavefront path tracer did not drain its ray queue");
         HIP_TRY(hippt::wf_launch_extend(W, cur, blocks, cnt, c.stream));
-        HIP_TRY(hippt::wf_launch_shade(W, cur, shadeSort, c.stream));
+        HIP_TRY(hippt::wf_launch_shade(W, cur, c.stream));
         HIP_TRY(hippt::wf_launch_generate(W, cur ^ 1, true, c.stream, allInFlight));
         cur ^= 1;
         if (it % kPollEvery != kPollEvery - 1) continue;
@@ -1483,10 +1481,6 @@ extern "C" bool hipptSetOption(int key, long long value) {
         if (value < -1 || value > 1) return false;
         s.fuseCombine = int(value);
         return true;
-    case HIPPT_OPT_SHADE_SORT:
-        if (value < -1 || value > 1) return false;
-        s.shadeSort = int(value);
-        return true;
     default: return false;
     }
 }
@@ -1526,7 +1520,6 @@ extern "C" long long hipptGetOption(int key) {
     case HIPPT_OPT_PIXEL_FORMAT: return s.pixelFormat;
     case HIPPT_OPT_CAMERA_POOL: return s.cameraPool;
     case HIPPT_OPT_FUSE_COMBINE: return s.fuseCombine;
-    case HIPPT_OPT_SHADE_SORT: return s.shadeSort;
     case HIPPT_INFO_LDS_TOP_BYTES: return s.activeTopBytes;
     case HIPPT_INFO_BLOCKS_PER_CU: return s.activeBlocksPerCu;
     default: return -1;

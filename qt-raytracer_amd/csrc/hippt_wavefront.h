@@ -49,8 +49,7 @@ hipError_t wf_launch_init(const WfParams &W, hipStream_t s);
 // one block per shard only counts the finished samples
 hipError_t wf_launch_generate(const WfParams &W, int nxt, bool countSamples, hipStream_t s, bool countOnly = false);
 hipError_t wf_launch_extend(const WfParams &W, int cur, int blocks, bool countTraversal, hipStream_t s);
-// sort: partition each block's entries by material kind first (general kernel only)
-hipError_t wf_launch_shade(const WfParams &W, int cur, bool sort, hipStream_t s);
+hipError_t wf_launch_shade(const WfParams &W, int cur, hipStream_t s);
 int wf_extend_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,
                             int ldsTris, unsigned topBytes = 0);
 

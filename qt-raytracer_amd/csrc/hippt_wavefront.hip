@@ -206,59 +206,12 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
     }
 }
 
-// The block's queue entries reordered by what their shading runs (SORT, the general kernel):
-// misses (sky), then Lambertian, Metal and Dielectric hits, so that a wave's lanes take one
-// material branch instead of all of them (a counting sort in LDS; §8(f1)'s "sorting by
-// material").  Every thread of the block calls it; returns this thread's entry (kNone past the
-// block's entries).  The order of the queues does not enter any path's arithmetic.
-constexpr int kShadeKinds = 4;
-__device__ __forceinline__ unsigned shade_partition(const WfParams &W, unsigned slot, unsigned *cnt, unsigned *sorted) {
-    const MeshParams &P = W.mp;
-    unsigned key = kShadeKinds;  // no entry: sorts last
-    if (slot != kNone) {
-        const int tri = __float_as_int(W.st[4 * size_t(slot) + 3].y);
-        if (tri < 0) {
-            key = 0;
-        } else {
-            const int m = __float_as_int(P.shade[tri].w) & ~kShadeSphere;
-            key = 1u + unsigned(__float_as_int(P.mats[2 * m].w));
-        }
-    }
-    const unsigned wave = threadIdx.x >> 6, nw = kWfBlock / 64;
-    unsigned long long mine = 0;
-#pragma unroll
-    for (int k = 0; k < kShadeKinds; ++k) {
-        const unsigned long long m = __ballot(key == unsigned(k));
-        if (key == unsigned(k)) mine = m;
-        if (__lane_id() == 0) cnt[k * nw + wave] = unsigned(__popcll(m));
-    }
-    __syncthreads();
-    if (threadIdx.x == 0) {  // exclusive prefix in (kind, wave) order
-        unsigned tot = 0;
-        for (unsigned i = 0; i < kShadeKinds * nw; ++i) {
-            const unsigned c = cnt[i];
-            cnt[i] = tot;
-            tot += c;
-        }
-        cnt[kShadeKinds * nw] = tot;
-    }
-    __syncthreads();
-    if (key < kShadeKinds) {
-        const unsigned rank = __builtin_amdgcn_mbcnt_hi(unsigned(mine >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(mine), 0u));
-        sorted[cnt[key * nw + wave] + rank] = slot;
-    }
-    __syncthreads();
-    return threadIdx.x < cnt[kShadeKinds * nw] ? sorted[threadIdx.x] : kNone;
-}
-
 // Shade and generate keep every shard an independent pipeline: block b works on shard
 // b % kWfShards and appends back to the same shard, so a shard never holds more than its
 // initial ceil(slots / kWfShards) entries.
-template <bool FULL, bool SORT>
+template <bool FULL>
 __global__ __launch_bounds__(kWfBlock) void wf_shade(WfParams W, int cur) {
     __shared__ unsigned lds[kWfBlock / 64 + 1];
-    __shared__ unsigned cnt[SORT ? kShadeKinds * (kWfBlock / 64) + 1 : 1];
-    __shared__ unsigned sorted[SORT ? kWfBlock : 1];
     const MeshParams &P = W.mp;
     if (blockIdx.x == 0 && threadIdx.x < kWfShards) W.ctr[ctr_word(kCtrFetch + int(threadIdx.x))] = 0;
     const unsigned shard = blockIdx.x % kWfShards;
@@ -269,9 +222,9 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(WfParams W, int cur) {
     if (first >= count) return;
     const unsigned local = first + threadIdx.x;
     bool again = false, finished = false;
-    unsigned slot = local < count ? (cur ? W.extQ1 : W.extQ0)[shard * W.shardCap + local] : kNone;
-    if (SORT) slot = shade_partition(W, slot, cnt, sorted);
-    if (slot != kNone) {
+    unsigned slot = kNone;
+    if (local < count) {
+        slot = (cur ? W.extQ1 : W.extQ0)[shard * W.shardCap + local];
         const float4 *p = W.st + 4 * size_t(slot);
         const float4 a = p[0], b = p[1], c = p[2], h = p[3];
         Slot q;
@@ -398,9 +351,8 @@ hipError_t wf_launch_extend(const WfParams &W, int cur, int blocks, bool countTr
     return hipGetLastError();
 }
 
-hipError_t wf_launch_shade(const WfParams &W, int cur, bool sort, hipStream_t s) {
-    const auto fn = !W.mp.full ? wf_shade<false, false> : sort ? wf_shade<true, true> : wf_shade<true, false>;
-    hipLaunchKernelGGL(fn, dim3(shard_grid(W)), dim3(kWfBlock), 0, s, W, cur);
+hipError_t wf_launch_shade(const WfParams &W, int cur, hipStream_t s) {
+    hipLaunchKernelGGL(W.mp.full ? wf_shade<true> : wf_shade<false>, dim3(shard_grid(W)), dim3(kWfBlock), 0, s, W, cur);
     return hipGetLastError();
 }
 

@@ -30,7 +30,7 @@ def pt():
                  (hippt.OPT_STACK_CAP, 0), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_LDS_TOP_NODES, -1),
                  (hippt.OPT_RNG_TABLE, 0), (hippt.OPT_BVH_COLLAPSE, -1), (hippt.OPT_BVH_NODE_COST, 200),
                  (hippt.OPT_BVH_LEAF4, 4), (hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_ARGB),
-                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1), (hippt.OPT_SHADE_SORT, -1)):
+                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1)):
         t.setOption(k, v)
     t.resetStats()
     yield t
@@ -134,30 +134,6 @@ def test_wavefront_matches_oracle(pt, name, w, h, spp, depth, slots, width, cap)
     _assert_same(px, acc, ora_px, ora_acc)
     st = pt.stats()
     assert st["segments"] == segs and st["pixelSamples"] == samples
-
-
-@pytest.mark.parametrize("name,w,h,spp,slots", [
-    ("random_scene", 96, 54, 4, 1 << 20),    # spheres: Lambertian, Metal, Dielectric
-    ("cornell_mixed", 96, 54, 4, 1 << 20),   # triangles, all three kinds
-    ("random_scene", 61, 37, 3, 3000),       # small pool: blocks of mixed and partial queues
-])
-def test_wavefront_shade_sort_matches_oracle(pt, name, w, h, spp, slots):
-    """HIPPT_OPT_SHADE_SORT: each wf_shade block orders its entries by material kind before
-    shading; the image and the counts are the oracle's with it on and off."""
-    sc = scenes.get_scene(name)
-    pt.uploadMesh(sc)
-    pt.setOption(hippt.OPT_PATH_MODE, 1)
-    pt.setOption(hippt.OPT_WAVEFRONT_SLOTS, slots)
-    ora_px, ora_acc, segs, samples = po.MeshScene(sc, w, h).frames(0, spp, 8)
-    for sort in (1, 0):
-        pt.setOption(hippt.OPT_SHADE_SORT, sort)
-        assert pt.initialize(w, h), pt.lastError()
-        assert pt.renderFrames(spp, 8), pt.lastError()
-        px, acc = pt.readback()
-        _assert_same(px, acc, ora_px, ora_acc)
-        st = pt.stats()
-        assert st["segments"] == segs and st["pixelSamples"] == samples
-        pt.resetStats()
 
 
 @pytest.mark.parametrize("slots", [1 << 21, 1 << 24])
