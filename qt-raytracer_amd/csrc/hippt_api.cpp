@@ -558,13 +558,15 @@ bool run_wavefront(Ctx &c, hippt::MeshParams p, bool cnt, bool spills, int spill
     W.slots = slots;
     W.shardCap = shardCap;
     W.ctr = c.wfCtr;
-    auto *base = static_cast<uint32_t *>(c.wfPool);
-    // slot records, then 3 sharded queues
-    W.st = reinterpret_cast<float4 *>(base);
-    uint32_t *queues = base + size_t(hippt::kWfStateWords) * slots;
-    W.extQ0 = queues;
-    W.extQ1 = queues + size_t(hippt::kWfShards) * shardCap;
-    W.genQ = queues + 2 * size_t(hippt::kWfShards) * shardCap;
+    // the two ray queues' payload arrays (float4 each), then the hit array
+    auto *base = static_cast<float4 *>(c.wfPool);
+    const size_t entries = size_t(hippt::kWfShards) * shardCap;
+    for (int q = 0; q < 2; ++q) {
+        W.ra[q] = base + (3 * q + 0) * entries;
+        W.rb[q] = base + (3 * q + 1) * entries;
+        W.rc[q] = base + (3 * q + 2) * entries;
+    }
+    W.hit = reinterpret_cast<float2 *>(base + 6 * entries);
     const bool wide = p.wide != 0, quant = p.wide == 2;
     const long long occKey = occupancy_key(s.scene.version, p.stackDepth, p.ldsScene != 0, p.full != 0, wide, quant) ^
                              ((long long)p.topBytes << 40);
@@ -585,13 +587,13 @@ bool run_wavefront(Ctx &c, hippt::MeshParams p, bool cnt, bool spills, int spill
     if (!next_events(c, ev, err)) return false;
     HIP_TRY(hipEventRecord(ev.a, c.stream));
     HIP_TRY(hippt::wf_launch_init(W, c.stream));
-    HIP_TRY(hippt::wf_launch_generate(W, 0, false, c.stream));
+    HIP_TRY(hippt::wf_launch_generate(W, 0, c.stream));
     // every path needs <= maxDepth extend rounds; slots regenerate as paths end
     const long long maxIter = (long long)p.maxDepth * ((p.totalItems + slots - 1) / slots + 1) + 64;
-    // Every kPollEvery iterations the ray-queue sizes are copied to pinned memory; the host
-    // reads the snapshot one batch later, so the stream always holds a batch of queued work.
-    // Iterations after the queue drained are no-ops (empty queues).
-    constexpr int kPollEvery = 8, kSnap = hippt::kWfShards * hippt::kCtrStride;
+    // Every kPollEvery iterations the ray-queue sizes (appended + generated entries) are copied to
+    // pinned memory; the host reads the snapshot one batch later, so the stream always holds a
+    // batch of queued work.  Iterations after the queue drained are no-ops (empty queues).
+    constexpr int kPollEvery = 8, kSnap = 2 * hippt::kWfShards * hippt::kCtrStride;
     if (!c.wfHost) HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c.wfHost), 2 * kSnap * sizeof(unsigned)));
     for (hipEvent_t &e : c.wfPoll)
         if (!e) HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
@@ -606,17 +608,17 @@ bool run_wavefront(Ctx &c, hippt::MeshParams p, bool cnt, bool spills, int spill
         if (it > maxIter) return fail(err, "wavefront path tracer did not drain its ray queue");
         HIP_TRY(hippt::wf_launch_extend(W, cur, blocks, cnt, c.stream));
         HIP_TRY(hippt::wf_launch_shade(W, cur, c.stream));
-        HIP_TRY(hippt::wf_launch_generate(W, cur ^ 1, true, c.stream, allInFlight));
+        if (!allInFlight) HIP_TRY(hippt::wf_launch_generate(W, cur ^ 1, c.stream));
         cur ^= 1;
         if (it % kPollEvery != kPollEvery - 1) continue;
         const int b = int(it / kPollEvery) & 1;
-        HIP_TRY(hipMemcpyAsync(c.wfHost + b * kSnap, c.wfCtr + hippt::ctr_word(hippt::kCtrExt0 + cur * hippt::kWfShards),
+        HIP_TRY(hipMemcpyAsync(c.wfHost + b * kSnap, c.wfCtr + hippt::ctr_word(hippt::ctr_queue(cur)),
                                kSnap * sizeof(unsigned), hipMemcpyDeviceToHost, c.stream));
         HIP_TRY(hipEventRecord(c.wfPoll[b], c.stream));
         if (it < 2 * kPollEvery - 1) continue;
         HIP_TRY(hipEventSynchronize(c.wfPoll[b ^ 1]));
         unsigned left = 0;
-        for (int k = 0; k < hippt::kWfShards; ++k) left += c.wfHost[(b ^ 1) * kSnap + k * hippt::kCtrStride];
+        for (int k = 0; k < 2 * hippt::kWfShards; ++k) left += c.wfHost[(b ^ 1) * kSnap + k * hippt::kCtrStride];
         if (left == 0) break;
     }
     HIP_TRY(hipEventRecord(ev.b, c.stream));

@@ -5,11 +5,12 @@
 
 namespace hippt {
 
-// Path-state pool: one 64-byte record (four float4) per slot.  Queue entries point at slots
-// in an order that scrambles as paths end and compact, so a record costs one cache line per
-// lane where separate arrays would cost one line per field.
-//   [0] ox oy oz dx   [1] dy dz tr tg   [2] tb rng depth item   [3] hitT hitI - -
-constexpr int kWfStateWords = 16;
+// Ray queues with their payload: queue q's entry i is a path's state in three float4 arrays,
+//   ra[q][i] = ox oy oz dx   rb[q][i] = dy dz tr tg   rc[q][i] = tb rng depth item,
+// and hit[i] = (t, primitive) of queue cur's entry i after wf_extend.  wf_shade appends a
+// scattered path to the other queue in block order, so every kernel reads and writes these
+// arrays in whole cache lines (no slot indirection: a scrambled slot order cost a line per lane).
+constexpr int kWfWordsPerSlot = 2 * 3 * 4 + 2;
 
 // Queues are split into kWfShards segments, each with its own counter; a 1024-thread block
 // appends to segment blockIdx % kWfShards with one atomic (contention on one counter word
@@ -17,37 +18,35 @@ constexpr int kWfStateWords = 16;
 constexpr int kWfShards = 8;
 constexpr int kWfBlock = 1024;
 
-// Device counters (W.ctr): ray-queue shard sizes (double-buffered), regenerate-queue shard
-// sizes, the extend kernel's per-shard fetch counters, and the work-item base.  Counter c
-// lives at word c * kCtrStride: one 128-byte line each, so atomics on different counters do
-// not serialise on a shared line.
+// Device counters (W.ctr): per queue, its shards' appended entries then the entries wf_generate
+// added after them; the extend kernel's per-shard fetch counters; the work items generated so
+// far.  Counter c lives at word c * kCtrStride: one 128-byte line each, so atomics on different
+// counters do not serialise on a shared line.
 enum {
-    kCtrExt0 = 0,
-    kCtrExt1 = kWfShards,
-    kCtrGen = 2 * kWfShards,
-    kCtrFetch = 3 * kWfShards,
-    kCtrWork = 4 * kWfShards,
-    kCtrCount = 4 * kWfShards + 1
+    kCtrFetch = 4 * kWfShards,
+    kCtrWork = 5 * kWfShards,
+    kCtrCount = 5 * kWfShards + 1
 };
+__host__ __device__ constexpr int ctr_queue(int q) { return 2 * kWfShards * q; }
+__host__ __device__ constexpr int ctr_gen(int q) { return 2 * kWfShards * q + kWfShards; }
 constexpr int kCtrStride = 32;
 constexpr int kCtrWords = kCtrCount * kCtrStride;
 __host__ __device__ constexpr int ctr_word(int c) { return c * kCtrStride; }
 
 struct WfParams {
     MeshParams mp;  // scene, camera, image band, batch, scratch, stats
-    float4 *st;  // slots records
-    unsigned *extQ0, *extQ1, *genQ;  // kWfShards segments of shardCap entries each
+    float4 *ra[2], *rb[2], *rc[2];  // the two ray queues' payload (kWfShards segments of shardCap)
+    float2 *hit;
     unsigned *ctr;
     unsigned slots, shardCap;
 };
 
-// Words of the pool: state + three queues of kWfShards segments of ceil(slots/kWfShards).
+// Words of the queues: 2 x 3 float4 + the hit float2 per entry, kWfShards segments of
+// ceil(slots/kWfShards) entries.
 size_t wf_pool_words(unsigned slots, unsigned *shardCap);
 hipError_t wf_launch_init(const WfParams &W, hipStream_t s);
-// countSamples: the regenerate queue holds finished samples (false for the initial fill).
-// countOnly: nothing is left to generate (every work item of the batch was generated up front);
-// one block per shard only counts the finished samples
-hipError_t wf_launch_generate(const WfParams &W, int nxt, bool countSamples, hipStream_t s, bool countOnly = false);
+// New paths into queue nxt's free capacity while work items remain.
+hipError_t wf_launch_generate(const WfParams &W, int nxt, hipStream_t s);
 hipError_t wf_launch_extend(const WfParams &W, int cur, int blocks, bool countTraversal, hipStream_t s);
 hipError_t wf_launch_shade(const WfParams &W, int cur, hipStream_t s);
 int wf_extend_blocks_per_cu(bool countTraversal, bool full, bool wide, bool quant, int stackDepth, int ldsNodes,

@@ -19,16 +19,16 @@ namespace hippt {
 namespace {
 using namespace trace;
 
-// Slot record fields (see WfParams::st).
-struct Slot {
+// A path's state as it sits in a ray queue (WfParams::ra/rb/rc, three float4 arrays per queue).
+struct Path {
     Ray r;
     float tr, tg, tb;
     uint32_t rng, item;
     int depth;
 };
 
-__device__ __forceinline__ void load_ray(const WfParams &W, unsigned s, Ray &r) {
-    const float4 a = W.st[4 * size_t(s)], b = W.st[4 * size_t(s) + 1];
+__device__ __forceinline__ void load_ray(const WfParams &W, int q, unsigned i, Ray &r) {
+    const float4 a = W.ra[q][i], b = W.rb[q][i];
     r.ox = a.x;
     r.oy = a.y;
     r.oz = a.z;
@@ -37,35 +37,21 @@ __device__ __forceinline__ void load_ray(const WfParams &W, unsigned s, Ray &r) 
     r.dz = b.y;
 }
 
-// whole: also the hit row (zeros), so that the record's 64 bytes are written at once.  wf_generate's
-// fresh records: 3.9 -> 2.8 ms for 132.7 M camera rays (r3ac; a partly written line is merged by the
-// memory side); wf_shade: no gain (+0.7%), its records' lines were read just before.
-__device__ __forceinline__ void store_slot(const WfParams &W, unsigned s, const Slot &q, bool whole = false) {
-    float4 *p = W.st + 4 * size_t(s);
-    p[0] = make_float4(q.r.ox, q.r.oy, q.r.oz, q.r.dx);
-    p[1] = make_float4(q.r.dy, q.r.dz, q.tr, q.tg);
-    p[2] = make_float4(q.tb, __uint_as_float(q.rng), __int_as_float(q.depth), __uint_as_float(q.item));
-    if (whole) p[3] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+__device__ __forceinline__ void store_path(const WfParams &W, int q, unsigned i, const Path &p) {
+    W.ra[q][i] = make_float4(p.r.ox, p.r.oy, p.r.oz, p.r.dx);
+    W.rb[q][i] = make_float4(p.r.dy, p.r.dz, p.tr, p.tg);
+    W.rc[q][i] = make_float4(p.tb, __uint_as_float(p.rng), __int_as_float(p.depth), __uint_as_float(p.item));
 }
 
-// Shard sizes of one sharded queue (counters first .. first + kWfShards - 1) and their prefix.
-struct Shards {
-    unsigned pre[kWfShards + 1];
-};
-
-__device__ __forceinline__ Shards load_shards(const unsigned *ctr, int first) {
-    Shards s;
-    s.pre[0] = 0;
-#pragma unroll
-    for (int k = 0; k < kWfShards; ++k) s.pre[k + 1] = s.pre[k] + ctr[ctr_word(first + k)];
-    return s;
+// Entries of queue q's shard k: appended by wf_shade plus added by wf_generate.
+__device__ __forceinline__ unsigned shard_size(const unsigned *ctr, int q, int k) {
+    return ctr[ctr_word(ctr_queue(q) + k)] + ctr[ctr_word(ctr_gen(q) + k)];
 }
 
-// Block-aggregated append (one atomic per block) to shard blockIdx % kWfShards of the queue
-// whose counters start at `first`.  Every thread of the block must call it (it synchronises);
-// `lds` holds kWfBlock/64 + 1 words.
-__device__ __forceinline__ void block_append(bool req, unsigned value, unsigned *q, unsigned cap, unsigned *ctr,
-                                             int first, unsigned *lds) {
+// Block-aggregated append (one atomic per block) to shard blockIdx % kWfShards of queue q:
+// returns this thread's entry index (kNone for a thread that does not append).  Every thread of
+// the block must call it (it synchronises); `lds` holds kWfBlock/64 + 1 words.
+__device__ __forceinline__ unsigned block_append(bool req, unsigned cap, unsigned *ctr, int q, unsigned *lds) {
     const unsigned long long m = __ballot(req);
     const unsigned wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
     const unsigned rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
@@ -79,26 +65,19 @@ __device__ __forceinline__ void block_append(bool req, unsigned value, unsigned 
             tot += c;
         }
         const unsigned shard = blockIdx.x % kWfShards;
-        lds[nw] = tot ? shard * cap + atomicAdd(&ctr[ctr_word(first + int(shard))], tot) : 0u;
+        lds[nw] = tot ? shard * cap + atomicAdd(&ctr[ctr_word(ctr_queue(q) + int(shard))], tot) : 0u;
     }
     __syncthreads();
-    if (req) q[lds[nw] + lds[wave] + rank] = value;
+    const unsigned at = req ? lds[nw] + lds[wave] + rank : kNone;
     __syncthreads();
+    return at;
 }
 
-// Initial regenerate queue: every slot, spread over the shards.
+// Counters of both queues and the work base start at 0.
+static_assert(kCtrCount <= 64, "wf_init clears the counters with one wave");
 __global__ void wf_init(WfParams W) {
-    const unsigned i = blockIdx.x * 256u + threadIdx.x;
-    const unsigned per = W.shardCap;
-    if (i < W.slots) W.genQ[(i / per) * W.shardCap + i % per] = i;
-    if (i < kWfShards) {
-        const unsigned lo = i * per, hi = min(W.slots, (i + 1) * per);
-        W.ctr[ctr_word(kCtrGen + i)] = hi > lo ? hi - lo : 0u;
-        W.ctr[ctr_word(kCtrExt0 + i)] = 0;
-        W.ctr[ctr_word(kCtrExt1 + i)] = 0;
-        W.ctr[ctr_word(kCtrFetch + i)] = 0;
-    }
-    if (i == 0) W.ctr[ctr_word(kCtrWork)] = 0;
+    const unsigned i = threadIdx.x;
+    if (i < unsigned(kCtrCount)) W.ctr[ctr_word(int(i))] = 0;
 }
 
 // WIDE: the megakernel's 4-wide traversal (QUANT: over 8-bit child boxes, global memory only).
@@ -111,18 +90,21 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
     constexpr bool TOP = WIDE && !LDS_SCENE;
     int *const stk = LDS_SCENE ? lds + P.numNodes * ldsNodeF4 * 4 : lds + (TOP ? (P.topBytes >> 2) : 0u);
     int *const my = stk + threadIdx.x;
-    const int qFirst = kCtrExt0 + cur * kWfShards;
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-        // this iteration's rays = its segments; consume the generated work; shade/generate
-        // of this iteration append to the other ray queue and the regenerate queue
-        const Shards rays = load_shards(W.ctr, qFirst), gen = load_shards(W.ctr, kCtrGen);
-        atomicAdd(&P.stats[0], (unsigned long long)rays.pre[kWfShards]);
-        W.ctr[ctr_word(kCtrWork)] += gen.pre[kWfShards];
+        // this iteration's rays = its segments; the paths wf_generate started into this queue
+        // = samples (every path of a batch ends within it) and advance the work base; this
+        // iteration's shade and generate fill the other queue (emptied here)
+        unsigned rays = 0, gen = 0;
 #pragma unroll
         for (int k = 0; k < kWfShards; ++k) {
-            W.ctr[ctr_word(kCtrExt0 + (cur ^ 1) * kWfShards + k)] = 0;
-            W.ctr[ctr_word(kCtrGen + k)] = 0;
+            rays += shard_size(W.ctr, cur, k);
+            gen += W.ctr[ctr_word(ctr_gen(cur) + k)];
+            W.ctr[ctr_word(ctr_queue(cur ^ 1) + k)] = 0;
+            W.ctr[ctr_word(ctr_gen(cur ^ 1) + k)] = 0;
         }
+        atomicAdd(&P.stats[0], (unsigned long long)rays);
+        if (gen) atomicAdd(&P.stats[1], (unsigned long long)gen);
+        W.ctr[ctr_word(kCtrWork)] += gen;
     }
     const float4 *nodes = P.nodes, *tris = P.tris;
     if (LDS_SCENE) {
@@ -146,13 +128,13 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
     }
     constexpr int nodeF4 = WIDE ? (QUANT ? 4 : (LDS_SCENE ? kLdsNode4F4 : 8)) : (LDS_SCENE ? kLdsNodeF4 : 4);
     const SpillArea S{P.spill, (blockIdx.x * unsigned(kMeshBlock) + threadIdx.x) * unsigned(P.spillCap), P.stackCap};
-    const unsigned *queue = cur ? W.extQ1 : W.extQ0;
     // each wave drains its block's home shard first, then the others in turn (one fetch
-    // counter per shard spreads the atomics over kWfShards lines)
+    // counter per shard spreads the atomics over kWfShards lines); consecutive lanes take
+    // consecutive entries, so the ray and hit arrays are read and written in whole lines
     unsigned fs = blockIdx.x % kWfShards, left = kWfShards;
-    unsigned fsCount = W.ctr[ctr_word(qFirst + int(fs))];
+    unsigned fsCount = shard_size(W.ctr, cur, int(fs));
     unsigned poolNext = 0, poolEnd = 0;
-    unsigned slot = kNone;
+    unsigned slot = kNone;  // this lane's queue entry
     bool need = true;
     Ray r{};
     Trav T;
@@ -170,14 +152,14 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
                 wave_fetch(need, poolNext, poolEnd, &W.ctr[ctr_word(kCtrFetch + int(fs))], unsigned(P.chunk), fsCount);
             if (need && qi != kNone) {
                 need = false;
-                slot = queue[fs * W.shardCap + qi];
-                load_ray(W, slot, r);
+                slot = fs * W.shardCap + qi;
+                load_ray(W, cur, slot, r);
                 prepare(r);
                 begin(T);
             }
             if (__ballot(need)) {  // this shard is drained
                 fs = fs + 1 == kWfShards ? 0u : fs + 1;
-                fsCount = W.ctr[ctr_word(qFirst + int(fs))];
+                fsCount = shard_size(W.ctr, cur, int(fs));
                 poolNext = poolEnd = 0;
                 --left;
             }
@@ -192,7 +174,7 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
                 traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
         } while (__popcll(__ballot(busy(T))) > unsigned(P.waveThreshold));
         if (slot != kNone && !busy(T)) {
-            *reinterpret_cast<float2 *>(W.st + 4 * size_t(slot) + 3) = make_float2(T.bestT, __int_as_float(T.bestI));
+            W.hit[slot] = make_float2(T.bestT, __int_as_float(T.bestI));
             slot = kNone;
             need = true;
         }
@@ -207,8 +189,8 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
 }
 
 // Shade and generate keep every shard an independent pipeline: block b works on shard
-// b % kWfShards and appends back to the same shard, so a shard never holds more than its
-// initial ceil(slots / kWfShards) entries.
+// b % kWfShards of queue cur and appends to the same shard of the other queue, so a shard never
+// holds more than its ceil(slots / kWfShards) entries.
 template <bool FULL>
 __global__ __launch_bounds__(kWfBlock) void wf_shade(WfParams W, int cur) {
     __shared__ unsigned lds[kWfBlock / 64 + 1];
@@ -216,18 +198,17 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(WfParams W, int cur) {
     if (blockIdx.x == 0 && threadIdx.x < kWfShards) W.ctr[ctr_word(kCtrFetch + int(threadIdx.x))] = 0;
     const unsigned shard = blockIdx.x % kWfShards;
     const unsigned first = (blockIdx.x / kWfShards) * kWfBlock;
-    const unsigned count = W.ctr[ctr_word(kCtrExt0 + cur * kWfShards + int(shard))];
+    const unsigned count = shard_size(W.ctr, cur, int(shard));
     // the grid covers a full shard; blocks past this iteration's queue leave before the appends
     // (block-uniform: no thread of such a block appends, so none needs the barriers)
     if (first >= count) return;
     const unsigned local = first + threadIdx.x;
     bool again = false, finished = false;
-    unsigned slot = kNone;
+    Path q{};
     if (local < count) {
-        slot = (cur ? W.extQ1 : W.extQ0)[shard * W.shardCap + local];
-        const float4 *p = W.st + 4 * size_t(slot);
-        const float4 a = p[0], b = p[1], c = p[2], h = p[3];
-        Slot q;
+        const unsigned i = shard * W.shardCap + local;
+        const float4 a = W.ra[cur][i], b = W.rb[cur][i], c = W.rc[cur][i];
+        const float2 h = W.hit[i];
         q.r.ox = a.x;
         q.r.oy = a.y;
         q.r.oz = a.z;
@@ -249,54 +230,48 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(WfParams W, int cur) {
             finished = true;
         } else if (scatter<FULL, false>(q.r, h.x, tri, P.shade, P.tris, P.mats, q.rng, q.tr, q.tg, q.tb, nullptr,
                                         P.rngTable)) {
-            store_slot(W, slot, q);
             again = true;
         } else {
             finished = true;  // absorbed: contributes 0
         }
-        if (finished) {
-            store_radiance(P.scratch, q.item, L0, L1, L2);
-        }
+        if (finished) store_radiance(P.scratch, q.item, L0, L1, L2);
     }
-    block_append(again, slot, cur ? W.extQ0 : W.extQ1, W.shardCap, W.ctr, kCtrExt0 + (cur ^ 1) * kWfShards, lds);
-    block_append(finished, slot, W.genQ, W.shardCap, W.ctr, kCtrGen, lds);
+    const unsigned at = block_append(again, W.shardCap, W.ctr, cur ^ 1, lds);
+    if (again) store_path(W, cur ^ 1, at, q);
 }
 
-__global__ __launch_bounds__(kWfBlock) void wf_generate(WfParams W, int nxt, int countSamples) {
-    __shared__ unsigned lds[kWfBlock / 64 + 1];
+// New paths into the free capacity of queue nxt (after this iteration's shade), work items in
+// order: shard k's share starts after the lower shards' (no atomics); W.ctr[kCtrWork] = items
+// generated so far (advanced by the next wf_extend, which reads the shards' counts).
+__global__ __launch_bounds__(kWfBlock) void wf_generate(WfParams W, int nxt) {
     const MeshParams &P = W.mp;
-    const Shards sh = load_shards(W.ctr, kCtrGen);
-    const unsigned count = sh.pre[kWfShards];
-    if (countSamples && blockIdx.x == 0 && threadIdx.x == 0 && count)
-        atomicAdd(&P.stats[1], (unsigned long long)count);  // the regenerate queue = finished samples
-    const unsigned shard = blockIdx.x % kWfShards;
-    const unsigned local = (blockIdx.x / kWfShards) * kWfBlock + threadIdx.x;
-    // work items in queue order: base + (entries of lower shards) + position in this shard
-    unsigned lower = 0, here = 0;
+    const unsigned base = W.ctr[ctr_word(kCtrWork)];
+    const unsigned left = P.totalItems - min(base, P.totalItems);
+    unsigned lower = 0, here = 0, used = 0;
 #pragma unroll
     for (int k = 0; k < kWfShards; ++k) {
-        if (unsigned(k) == shard) {
-            lower = sh.pre[k];
-            here = sh.pre[k + 1] - sh.pre[k];
+        const unsigned n = W.ctr[ctr_word(ctr_queue(nxt) + k)];
+        const unsigned gen = min(W.shardCap - min(n, W.shardCap), left - min(lower, left));
+        if (unsigned(k) == blockIdx.x % kWfShards) {
+            here = gen;
+            used = n;
+            break;
         }
+        lower += gen;
     }
-    const unsigned base = W.ctr[ctr_word(kCtrWork)];  // advanced by the next wf_extend
-    // blocks with nothing to generate leave before the appends (block-uniform, see wf_shade)
-    const unsigned first = local - threadIdx.x;
-    if (first >= here || base + lower + first >= P.totalItems) return;
-    const bool ok = local < here && base + lower + local < P.totalItems;
-    unsigned slot = kNone;
-    if (ok) {
-        const unsigned item = base + lower + local;
-        slot = W.genQ[shard * W.shardCap + local];
-        Slot q;
-        camera_sample(P, item, q.r, q.rng);
+    const unsigned local = (blockIdx.x / kWfShards) * kWfBlock + threadIdx.x;
+    if (local < here) {
+        const unsigned shard = blockIdx.x % kWfShards;
+        Path q;
+        q.item = base + lower + local;
+        camera_sample(P, q.item, q.r, q.rng);
         q.tr = q.tg = q.tb = 1.0f;
         q.depth = 0;
-        q.item = item;
-        store_slot(W, slot, q, true);
+        store_path(W, nxt, shard * W.shardCap + used + local, q);
     }
-    block_append(ok, slot, nxt ? W.extQ1 : W.extQ0, W.shardCap, W.ctr, kCtrExt0 + nxt * kWfShards, lds);
+    // the shard's count, computed alike by every block of the shard from values no block of
+    // this launch changes
+    if (local == 0) W.ctr[ctr_word(ctr_gen(nxt) + int(blockIdx.x % kWfShards))] = here;
 }
 
 using ExtFn = void (*)(WfParams, int);
@@ -314,24 +289,23 @@ ExtFn ext_fn(bool count, bool lds, bool full, bool wide, bool quant) {
 }  // namespace
 
 size_t wf_pool_words(unsigned slots, unsigned *shardCap) {
-    // shards are closed pipelines (wf_shade/wf_generate): shard k never holds more than the
-    // slots wf_init gave it
+    // shards are closed pipelines (wf_shade/wf_generate): shard k never holds more than cap
+    // entries
     const unsigned cap = (slots + kWfShards - 1) / kWfShards;
     *shardCap = cap;
-    return size_t(slots) * kWfStateWords + size_t(3) * kWfShards * cap;
+    return size_t(kWfShards) * cap * kWfWordsPerSlot;
 }
 
 // kWfShards blocks per 1024 entries of one shard segment
 static unsigned shard_grid(const WfParams &W) { return kWfShards * ((W.shardCap + kWfBlock - 1) / kWfBlock); }
 
 hipError_t wf_launch_init(const WfParams &W, hipStream_t s) {
-    hipLaunchKernelGGL(wf_init, dim3((W.slots + 255) / 256), dim3(256), 0, s, W);
+    hipLaunchKernelGGL(wf_init, dim3(1), dim3(64), 0, s, W);
     return hipGetLastError();
 }
 
-hipError_t wf_launch_generate(const WfParams &W, int nxt, bool countSamples, hipStream_t s, bool countOnly) {
-    hipLaunchKernelGGL(wf_generate, dim3(countOnly ? unsigned(kWfShards) : shard_grid(W)), dim3(kWfBlock), 0, s, W, nxt,
-                       countSamples ? 1 : 0);
+hipError_t wf_launch_generate(const WfParams &W, int nxt, hipStream_t s) {
+    hipLaunchKernelGGL(wf_generate, dim3(shard_grid(W)), dim3(kWfBlock), 0, s, W, nxt);
     return hipGetLastError();
 }
 

@@ -154,7 +154,7 @@ def test_wavefront_equals_megakernel_1080p(pt, slots):
 @pytest.mark.parametrize("slots,w,h,spp", [(None, 1920, 1080, 64), (1 << 28, 3840, 2160, 32)])
 def test_wavefront_large_pools_equal_megakernel(pt, slots, w, h, spp):
     """The default pool (2^27 slots: the whole 1080p/64 spp bench step in flight, one
-    generation) and the largest one (2^28 slots, 17 GB: a 4K/32 spp call) give the
+    generation) and the largest one (2^28 entries, 28 GB of queues: a 4K/32 spp call) give the
     megakernel's image bit for bit (the megakernel is oracle-checked above)."""
     sc = scenes.blob70k()
     pt.uploadMesh(sc)
