@@ -9,6 +9,7 @@
 //   * triangle-mesh scenes with a host-built SAH BVH in addition to the reference's
 //     built-in 4-sphere scene.
 #include "../../include/hippt.h"
+#include "item_order.h"
 
 #include <hip/hip_runtime.h>
 
@@ -36,7 +37,10 @@ namespace {
 
 using hippt::CameraF;
 
-constexpr int kStatWords = 32;  // [0..3] hipptStats counters, [4..19] phase profile, [20..24] hit-children histogram
+using hippt::kStatSlots;
+using hippt::kStatWords;
+constexpr size_t kStatBytes = size_t(kStatSlots) * kStatWords * sizeof(unsigned long long);
+
 
 // 4-wide traversal: LDS stack content capacity for scenes outside LDS (19 + 3 spare entries =
 // 22 KB per 256-lane block: 7 blocks per CU in 160 KB).
@@ -81,6 +85,13 @@ struct Ctx {
     float4 *nodes4q = nullptr; // the 4-wide BVH with 8-bit child boxes
     float4 *nodes4h = nullptr; // hybrid layout (float top + 8-bit nodes) for hybridTop top nodes
     int hybridTop = -1;
+    // the queues' pixel-run order of this context's rows (HIPPT_OPT_ITEM_ORDER), built per key
+    unsigned *runOrder = nullptr;
+    unsigned runCount = 0;
+    struct OrderKey {
+        int version = -1, width = 0, height = 0, y0 = 0, rows = 0, stride = 0, frames = 0;
+        CameraF cam{};
+    } orderKey;
     int *spill = nullptr;      // 4-wide traversal: per-lane stack spill area
     size_t spillBytes = 0;
     // wavefront path-state pool (allocated on first use)
@@ -157,6 +168,7 @@ struct State {
     int pixelFormat = HIPPT_PIXEL_ARGB;  // output frame words (HIPPT_OPT_PIXEL_FORMAT)
     int cameraPool = -1;  // megakernel camera-ray pool (HIPPT_OPT_CAMERA_POOL; -1: automatic)
     int fuseCombine = -1;  // combine inside the next megakernel launch (HIPPT_OPT_FUSE_COMBINE)
+    int itemOrder = -1;    // scene-hitting pixel runs first (HIPPT_OPT_ITEM_ORDER; -1: automatic)
     std::vector<std::pair<int, uint32_t *>> rngTables;  // per device, built on first use
     unsigned activeTopBytes = 0;  // of the last mesh render (hipptGetOption HIPPT_INFO_*)
     int activeBlocksPerCu = 0;
@@ -255,6 +267,10 @@ void free_scene_buffers(Ctx &c) {
     (void)hipFree(c.nodes4h);
     c.nodes = c.tris = c.shade = c.mats = c.nodes4 = c.nodes4q = c.nodes4h = nullptr;
     c.hybridTop = -1;
+    (void)hipFree(c.runOrder);
+    c.runOrder = nullptr;
+    c.runCount = 0;
+    c.orderKey = Ctx::OrderKey{};
     c.sceneVersion = -1;
 }
 
@@ -384,6 +400,37 @@ unsigned packed_ref_bits(int numNodes, int numPrims) {
 
 // The hybrid node layout (bvh_builder.h hybrid_bvh4) for `top` top-of-tree nodes: built on the
 // host once per (scene, top) and uploaded to the context's device.
+// The queues' pixel-run order of a context's rows for this scene, camera and image
+// (item_order.h), rebuilt on the host when one of them changes.
+bool ensure_order(Ctx &c, const CameraF &cam, int frames, const char **err) {
+    State &s = S();
+    Ctx::OrderKey key;
+    key.version = s.scene.version;
+    key.width = s.width;
+    key.height = s.height;
+    key.y0 = c.y0;
+    key.rows = c.rows;
+    key.stride = c.stride;
+    key.frames = frames;
+    key.cam = cam;
+    if (c.runOrder && std::memcmp(&key, &c.orderKey, sizeof key) == 0) return true;
+    std::vector<uint32_t> runs, order;
+    const size_t hits = hippt::build_run_order(s.scene.bvh4, reinterpret_cast<const float *>(s.scene.tris.data()), cam,
+                                               s.width, s.height, c.y0, c.rows, c.stride, runs);
+    hippt::build_item_table(runs, hits, unsigned(c.rows) * unsigned(s.width), unsigned(frames), hippt::kMeshQueues, order);
+    HIP_TRY(hipSetDevice(c.device));
+    HIP_TRY(hipStreamSynchronize(c.stream));  // launches in flight read the old order
+    (void)hipFree(c.runOrder);
+    c.runOrder = nullptr;
+    c.runCount = 0;
+    HIP_TRY(hipMalloc(&c.runOrder, std::max<size_t>(1, order.size()) * sizeof(unsigned)));
+    if (!order.empty())
+        HIP_TRY(hipMemcpy(c.runOrder, order.data(), order.size() * sizeof(unsigned), hipMemcpyHostToDevice));
+    c.runCount = unsigned(runs.size());
+    c.orderKey = key;
+    return true;
+}
+
 bool ensure_hybrid(Ctx &c, int top, const char **err) {
     State &s = S();
     SceneHost &sc = s.scene;
@@ -450,10 +497,10 @@ bool init_inner(int width, int height, const char **err) {
         HIP_TRY(hipMalloc(&c.accum, std::max<size_t>(16, px * sizeof(float4))));
         HIP_TRY(hipMalloc(&c.out, std::max<size_t>(16, px * sizeof(uint32_t))));
         HIP_TRY(hipMalloc(&c.queue, kQueueBytes));
-        HIP_TRY(hipMalloc(&c.stats, kStatWords * sizeof(unsigned long long)));
+        HIP_TRY(hipMalloc(&c.stats, kStatBytes));
         HIP_TRY(hipMemsetAsync(c.accum, 0, px * sizeof(float4), c.stream));
         HIP_TRY(hipMemsetAsync(c.out, 0, px * sizeof(uint32_t), c.stream));
-        HIP_TRY(hipMemsetAsync(c.stats, 0, kStatWords * sizeof(unsigned long long), c.stream));
+        HIP_TRY(hipMemsetAsync(c.stats, 0, kStatBytes, c.stream));
         HIP_TRY(hipDeviceGetAttribute(&c.cus, hipDeviceAttributeMultiprocessorCount, c.device));
         HIP_TRY(hipStreamSynchronize(c.stream));
     }
@@ -857,6 +904,14 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.refBits = ldsScene && wide ? packed_ref_bits(numNodes, numTris) : 0u;
                         p.rngTable = nullptr;
                         p.poolWords = poolWords;
+                        // Scene-hitting pixel runs first, the sky's last, per XCD queue (megakernel;
+                        // item_order.h).  Automatic for LDS-resident scenes (Cornell +0.3-1.0% at
+                        // full size); trees in global memory lose ~1% with it (blob70k, r5q/r5r)
+                        if (s.pathMode == 0 && (s.itemOrder == 1 || (s.itemOrder == -1 && ldsScene))) {
+                            if (!ensure_order(c, cam, nf, err)) return false;
+                            p.runOrder = c.runOrder;
+                            p.runCount = c.runCount;
+                        }
                         p.poolOffset = unsigned(hippt::mesh_lds_bytes(stackDepth, ldsScene ? numNodes : 0,
                                                                       ldsScene ? numTris : 0, wide, topBytes,
                                                                       ldsScene ? numMats : 0));
@@ -1323,6 +1378,17 @@ extern "C" bool hipptResetAccumulation(const char **err) {
     return true;
 }
 
+// A context's launch counters summed over their kStatSlots copies (hippt_device.h).
+bool read_stats(const Ctx &c, unsigned long long (&v)[kStatWords]) {
+    std::vector<unsigned long long> all(size_t(kStatSlots) * kStatWords);
+    std::memset(v, 0, sizeof(v));
+    if (hipSetDevice(c.device) != hipSuccess) return false;
+    if (hipMemcpy(all.data(), c.stats, kStatBytes, hipMemcpyDeviceToHost) != hipSuccess) return false;
+    for (int k = 0; k < kStatSlots; ++k)
+        for (int i = 0; i < kStatWords; ++i) v[i] += all[size_t(k) * kStatWords + size_t(i)];
+    return true;
+}
+
 // ---- counters / options -------------------------------------------------------------------------
 extern "C" bool hipptGetStats(hipptStats *out) {
     std::lock_guard<std::mutex> g(S().mu);
@@ -1332,9 +1398,8 @@ extern "C" bool hipptGetStats(hipptStats *out) {
     const char *err = nullptr;
     if (s.ready && !sync_locked(&err)) return false;
     for (Ctx &c : s.ctxs) {
-        unsigned long long v[4] = {0, 0, 0, 0};
-        if (hipSetDevice(c.device) != hipSuccess) return false;
-        if (hipMemcpy(v, c.stats, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return false;
+        unsigned long long v[kStatWords];
+        if (!read_stats(c, v)) return false;
         out->segments += v[0];
         out->pixelSamples += v[1];
         out->nodeVisits += v[2];
@@ -1361,8 +1426,7 @@ extern "C" int hipptGetCounters(unsigned long long *out, int n) {
     if (s.ready && !sync_locked(&err)) return 0;
     for (Ctx &c : s.ctxs) {
         unsigned long long v[kStatWords];
-        if (hipSetDevice(c.device) != hipSuccess) return 0;
-        if (hipMemcpy(v, c.stats, sizeof(v), hipMemcpyDeviceToHost) != hipSuccess) return 0;
+        if (!read_stats(c, v)) return 0;
         for (int i = 0; i < n; ++i) out[i] += v[i];
     }
     return n;
@@ -1375,7 +1439,7 @@ extern "C" void hipptResetStats(void) {
     if (s.ready) sync_locked(&err);
     for (Ctx &c : s.ctxs) {
         (void)hipSetDevice(c.device);
-        (void)hipMemset(c.stats, 0, kStatWords * sizeof(unsigned long long));
+        (void)hipMemset(c.stats, 0, kStatBytes);
     }
     s.traceMs = s.combineMs = 0;
     s.traceLaunches = s.combineLaunches = 0;
@@ -1483,6 +1547,10 @@ extern "C" bool hipptSetOption(int key, long long value) {
         if (value < -1 || value > 1) return false;
         s.fuseCombine = int(value);
         return true;
+    case HIPPT_OPT_ITEM_ORDER:
+        if (value < -1 || value > 1) return false;
+        s.itemOrder = int(value);
+        return true;
     default: return false;
     }
 }
@@ -1522,6 +1590,7 @@ extern "C" long long hipptGetOption(int key) {
     case HIPPT_OPT_PIXEL_FORMAT: return s.pixelFormat;
     case HIPPT_OPT_CAMERA_POOL: return s.cameraPool;
     case HIPPT_OPT_FUSE_COMBINE: return s.fuseCombine;
+    case HIPPT_OPT_ITEM_ORDER: return s.itemOrder;
     case HIPPT_INFO_LDS_TOP_BYTES: return s.activeTopBytes;
     case HIPPT_INFO_BLOCKS_PER_CU: return s.activeBlocksPerCu;
     default: return -1;

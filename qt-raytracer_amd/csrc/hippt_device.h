@@ -82,6 +82,11 @@ struct MeshParams {
     // LDS-resident 4-wide trees: low bits of a packed child key that carry the child's code
     // (trace::child_key_p; hippt_api.cpp packed_ref_bits)
     unsigned refBits;
+    // The queues' order of the batch's items (item_order.h build_item_table): queue position
+    // fl*bandPixels + 64*j + k is item runOrder[fl*runCount + j] + k for j < runCount (runs of 64
+    // band pixels per frame); null: image order.
+    const unsigned *runOrder;
+    unsigned runCount;
     // random_in_unit_sphere memoized (null: the rejection loop): entry 2^32-word table, see
     // launch_rng_table
     const uint32_t *rngTable;
@@ -134,6 +139,14 @@ constexpr int kPoolWordsPinhole = 5, kPoolWordsFull = 8;
 size_t mesh_lds_block_budget();
 size_t mesh_lds_scene_limit();
 constexpr int kMeshBlock = 256;
+// Launch counters (MeshParams::stats, Sphere4Params::stats): kStatSlots copies of kStatWords
+// words ([0..3] hipptStats counters, [4..19] phase profile, [20..24] hit-children histogram),
+// block b adding into copy b % kStatSlots; the host sums the copies.  One shared copy took every
+// wave's end-of-launch atomics on one cache line: ~50 us of each megakernel launch's tail
+// (7168 waves x 2), and ~0.3 ms of a 1080p legacy frame (32k waves).
+constexpr int kStatWords = 32, kStatSlots = 64;
+// megakernel work queues (one per XCD; hippt_trace.h queue_start splits the items evenly)
+constexpr unsigned kMeshQueues = 8;
 // LDS-resident scene copies: 2-wide nodes at an 80-byte stride, 4-wide nodes in the 128-byte
 // global layout (the octant row addressing by or/xor needs 128-byte alignment; a 144- or
 // 160-byte stride cut the LDS bank conflicts of node rows by 40% but not the kernel time, and

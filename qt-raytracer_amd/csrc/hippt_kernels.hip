@@ -159,7 +159,7 @@ __global__ __launch_bounds__(256) void sphere4_kernel(Sphere4Params P) {
         }
     }
     segs = wave_sum(segs);
-    if ((threadIdx.x & 63) == 0 && segs) atomicAdd(&P.stats[0], segs);
+    if ((threadIdx.x & 63) == 0 && segs) atomicAdd(&stat_slot(P.stats)[0], segs);
 }
 
 // =========================================================================================
@@ -393,7 +393,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                 }
                 if (n > avail) {
                     // the camera rays of the wave's next 64 items, every lane at once
-                    const unsigned it = queue_fetch(true, Q, P.queue, P.totalItems, P.chunk);
+                    const unsigned it = order_item(P, queue_fetch(true, Q, P.queue, P.totalItems, P.chunk));
 #ifdef HIPPT_DEBUG_TIMELINE
                     if (!tlDrained && __ballot(it == kNone)) tlDrained = __builtin_amdgcn_s_memrealtime();
                     tlItems += __popcll(__ballot(it != kNone));
@@ -430,7 +430,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                 }
             }
         } else if (__ballot(need)) {
-            const unsigned it = queue_fetch(need, Q, P.queue, P.totalItems, P.chunk);
+            const unsigned it = order_item(P, queue_fetch(need, Q, P.queue, P.totalItems, P.chunk));
 #ifdef HIPPT_DEBUG_TIMELINE
             if (!tlDrained && __ballot(need && it == kNone)) tlDrained = __builtin_amdgcn_s_memrealtime();
             tlItems += __popcll(__ballot(it != kNone));
@@ -536,19 +536,20 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         nvis = wave_sum(nvis);
         ntest = wave_sum(ntest);
     }
+    unsigned long long *const st = stat_slot(P.stats);
     if (__lane_id() == 0) {
-        atomicAdd(&P.stats[0], segsW);
-        atomicAdd(&P.stats[1], samplesW);
+        atomicAdd(&st[0], segsW);
+        atomicAdd(&st[1], samplesW);
         if (STATS) {
-            atomicAdd(&P.stats[2], nvis);
-            atomicAdd(&P.stats[3], ntest);
+            atomicAdd(&st[2], nvis);
+            atomicAdd(&st[3], ntest);
         }
     }
     if (STATS) {
 #pragma unroll
         for (int k = 0; k < kProfSlots; ++k) {
             const unsigned long long v = wave_sum(pc[k]);
-            if (__lane_id() == 0) atomicAdd(&P.stats[4 + k], v);
+            if (__lane_id() == 0) atomicAdd(&st[4 + k], v);
         }
     }
 }

@@ -107,6 +107,11 @@ __device__ __forceinline__ void divmod(unsigned n, unsigned d, float rcp, unsign
     r = unsigned(rem);
 }
 
+// This block's copy of the launch counters (kStatSlots).
+__device__ __forceinline__ unsigned long long *stat_slot(unsigned long long *stats) {
+    return stats + (blockIdx.x % unsigned(kStatSlots)) * unsigned(kStatWords);
+}
+
 __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
     return v;
@@ -143,7 +148,7 @@ __device__ __forceinline__ unsigned wave_fetch(bool req, unsigned &poolNext, uns
 // is within one chunk per wave of its end (a short tail), and a wave whose home queue is
 // drained moves on to the others.  Counters start at 0 and count dynamically claimed items.
 // (Claiming exactly the requesting lanes' count in the tail instead: neutral)
-constexpr unsigned kQueues = 8, kQueueStride = 32, kTailChunk = 64;
+constexpr unsigned kQueues = kMeshQueues, kQueueStride = 32, kTailChunk = 64;
 
 struct WorkQueue {
     unsigned g, left;  // current queue, queues not yet found drained
@@ -256,6 +261,17 @@ __device__ __forceinline__ void prepare(Ray &r) {
 
 // Camera sample for work item `it`: RenderWorker::render u/v (RayTracerFboItem.cpp:109-110) and
 // Camera::get_ray (RayTracer.h:563-567, disk draw always consumed).
+// The work item at queue position `it` (MeshParams::runOrder, item_order.h build_item_table):
+// the 64-item slot of (frame, run) handed out as the slot the table names, the offset within
+// the run kept; positions outside whole runs and kNone stay as they are.
+__device__ __forceinline__ unsigned order_item(const MeshParams &P, unsigned it) {
+    if (it == kNone || !P.runOrder) return it;
+    unsigned fl, q;
+    divmod(it, P.bandPixels, P.rcpBandPixels, fl, q);
+    const unsigned run = q >> 6;
+    return run < P.runCount ? P.runOrder[fl * P.runCount + run] + (q & 63u) : it;
+}
+
 __device__ __forceinline__ void camera_sample(const MeshParams &P, unsigned it, Ray &r, uint32_t &rng) {
     unsigned fl, p, yb, x;
     divmod(it, P.bandPixels, P.rcpBandPixels, fl, p);

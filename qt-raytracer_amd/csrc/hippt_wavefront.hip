@@ -182,8 +182,8 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
     if (STATS) {
         const unsigned long long a = wave_sum(nvis), b = wave_sum(ntest);
         if (__lane_id() == 0) {
-            atomicAdd(&P.stats[2], a);
-            atomicAdd(&P.stats[3], b);
+            atomicAdd(&stat_slot(P.stats)[2], a);
+            atomicAdd(&stat_slot(P.stats)[3], b);
         }
     }
 }

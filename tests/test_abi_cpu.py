@@ -88,6 +88,7 @@ def test_options_validate():
     (hippt.OPT_RNG_TABLE, (0, 1), (-1, 2), 0),
     (hippt.OPT_CAMERA_POOL, (-1, 0, 1), (-2, 2), -1),
     (hippt.OPT_FUSE_COMBINE, (-1, 0, 1), (-2, 2), -1),
+    (hippt.OPT_ITEM_ORDER, (-1, 0, 1), (-2, 2), -1),
     (hippt.OPT_STACK_CAP, (0, 4, 30), (3, 31), 0),
     (hippt.OPT_BVH_QUANT, (-1, 0, 1, 2), (-2, 3), -1),
 ])

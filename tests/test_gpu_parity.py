@@ -30,7 +30,7 @@ def pt():
                  (hippt.OPT_STACK_CAP, 0), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_LDS_TOP_NODES, -1),
                  (hippt.OPT_RNG_TABLE, 0), (hippt.OPT_BVH_COLLAPSE, -1), (hippt.OPT_BVH_NODE_COST, 200),
                  (hippt.OPT_BVH_LEAF4, 4), (hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_ARGB),
-                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1)):
+                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1), (hippt.OPT_ITEM_ORDER, -1)):
         t.setOption(k, v)
     t.resetStats()
     yield t
@@ -410,6 +410,34 @@ def test_camera_pool_does_not_change_results(pt, name, variant):
         st = pt.stats()
         assert st["segments"] == ora[2] and st["pixelSamples"] == ora[3]
         pt.resetStats()
+
+
+@pytest.mark.parametrize("name,w,h,frames", [("cornell34", 200, 77, 3), ("blob70k", 131, 64, 2),
+                                               ("cornell_mixed", 96, 53, 2)])
+def test_item_order_does_not_change_results(pt, name, w, h, frames):
+    """HIPPT_OPT_ITEM_ORDER: the queues hand out each XCD queue's scene-hitting 64-pixel runs first
+    and the sky's last (item_order.cpp); the image and the counts are the oracle's either way, for
+    bands whose pixel count is not a multiple of 64 and for interleaved rows."""
+    sc = scenes.get_scene(name)
+    ora = po.MeshScene(sc, w, h).frames(0, frames, 8)
+    pt.uploadMesh(sc)
+    for order in (1, 0, -1):
+        pt.setOption(hippt.OPT_ITEM_ORDER, order)
+        assert pt.initialize(w, h), pt.lastError()
+        assert pt.renderFrames(frames, 8), pt.lastError()
+        got = pt.readback()
+        _assert_same(got[0], got[1], ora[0], ora[1])
+        st = pt.stats()
+        assert st["segments"] == ora[2] and st["pixelSamples"] == ora[3]
+        pt.resetStats()
+    pt.setOption(hippt.OPT_ITEM_ORDER, 1)
+    pt.setRowInterleave(1, 3)
+    assert pt.initialize(w, h)
+    assert pt.renderFrames(frames, 8)
+    got = pt.readback()
+    rows = np.arange(1, h, 3)
+    _assert_same(got[0][rows], got[1][rows], ora[0][rows], ora[1][rows])
+    pt.setRowRange(0, 0)
 
 
 @pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene"])
