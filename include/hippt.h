@@ -231,10 +231,11 @@ enum {
                                        batch's launch on the same device (beside its paths) instead of as a
                                        launch of its own, whenever nothing reads the image in between (1), or
                                        never (0); -1 (default): automatic.  Same results either way */
-    , HIPPT_OPT_ITEM_ORDER = 28     /* megakernel: the work queues hand out each frame's runs of 64 pixels whose
-                                       camera rays hit the scene first and the sky's last, so the launch's
-                                       tail holds cheap samples (1), or in image order (0); -1 (default):
-                                       automatic (on for scenes held in LDS).  Same results either way */
+    , HIPPT_OPT_ITEM_ORDER = 28     /* megakernel: the work queues hand out runs of 64 pixels in order of an
+                                       estimated sample length (camera rays and a few bounce directions on
+                                       the host's tree), longest first, so that a wave's lanes hold samples
+                                       of similar length (1), or in image order (0); -1 (default): automatic
+                                       (on).  Same results either way */
 };
 /* Output frame word formats (HIPPT_OPT_PIXEL_FORMAT).  Both map an accumulated colour c to
  * sqrt(clamp(c, 0, 1)) per channel.

@@ -89,9 +89,12 @@ struct Ctx {
     unsigned *runOrder = nullptr;
     unsigned runCount = 0;
     struct OrderKey {
-        int version = -1, width = 0, height = 0, y0 = 0, rows = 0, stride = 0, frames = 0;
+        int version = -1, width = 0, height = 0, y0 = 0, rows = 0, stride = 0, maxDepth = 0;
         CameraF cam{};
-    } orderKey;
+    } orderKey;                  // of runCosts
+    std::vector<float> runCosts;  // per run of 64 band pixels (item_order.h run_costs)
+    bool runCostsValid = false;
+    int orderFrames = 0;          // batch size of the table in runOrder
     int *spill = nullptr;      // 4-wide traversal: per-lane stack spill area
     size_t spillBytes = 0;
     // wavefront path-state pool (allocated on first use)
@@ -271,6 +274,8 @@ void free_scene_buffers(Ctx &c) {
     c.runOrder = nullptr;
     c.runCount = 0;
     c.orderKey = Ctx::OrderKey{};
+    c.runCostsValid = false;
+    c.orderFrames = 0;
     c.sceneVersion = -1;
 }
 
@@ -398,11 +403,9 @@ unsigned packed_ref_bits(int numNodes, int numPrims) {
     return std::max(bits, 8u);
 }
 
-// The hybrid node layout (bvh_builder.h hybrid_bvh4) for `top` top-of-tree nodes: built on the
-// host once per (scene, top) and uploaded to the context's device.
-// The queues' pixel-run order of a context's rows for this scene, camera and image
-// (item_order.h), rebuilt on the host when one of them changes.
-bool ensure_order(Ctx &c, const CameraF &cam, int frames, const char **err) {
+// The queues' item table of a context's rows (item_order.h): run cost estimates per (scene,
+// camera, image, rows, depth), the table per batch size; rebuilt on the host when one changes.
+bool ensure_order(Ctx &c, const CameraF &cam, int frames, int maxDepth, const char **err) {
     State &s = S();
     Ctx::OrderKey key;
     key.version = s.scene.version;
@@ -411,26 +414,34 @@ bool ensure_order(Ctx &c, const CameraF &cam, int frames, const char **err) {
     key.y0 = c.y0;
     key.rows = c.rows;
     key.stride = c.stride;
-    key.frames = frames;
+    key.maxDepth = maxDepth;
     key.cam = cam;
-    if (c.runOrder && std::memcmp(&key, &c.orderKey, sizeof key) == 0) return true;
-    std::vector<uint32_t> runs, order;
-    const size_t hits = hippt::build_run_order(s.scene.bvh4, reinterpret_cast<const float *>(s.scene.tris.data()), cam,
-                                               s.width, s.height, c.y0, c.rows, c.stride, runs);
-    hippt::build_item_table(runs, hits, unsigned(c.rows) * unsigned(s.width), unsigned(frames), hippt::kMeshQueues, order);
+    const bool sameCosts = c.runCostsValid && std::memcmp(&key, &c.orderKey, sizeof key) == 0;
+    if (sameCosts && c.runOrder && c.orderFrames == frames) return true;
+    if (!sameCosts) {
+        hippt::run_costs(s.scene.bvh4, reinterpret_cast<const float *>(s.scene.tris.data()), cam, s.width, s.height,
+                         c.y0, c.rows, c.stride, maxDepth, c.runCosts);
+        c.orderKey = key;
+        c.runCostsValid = true;
+    }
+    std::vector<uint32_t> order;
+    hippt::build_item_table(c.runCosts, unsigned(c.rows) * unsigned(s.width), unsigned(frames), hippt::kMeshQueues,
+                            order);
     HIP_TRY(hipSetDevice(c.device));
-    HIP_TRY(hipStreamSynchronize(c.stream));  // launches in flight read the old order
+    HIP_TRY(hipStreamSynchronize(c.stream));  // launches in flight read the old table
     (void)hipFree(c.runOrder);
     c.runOrder = nullptr;
     c.runCount = 0;
     HIP_TRY(hipMalloc(&c.runOrder, std::max<size_t>(1, order.size()) * sizeof(unsigned)));
     if (!order.empty())
         HIP_TRY(hipMemcpy(c.runOrder, order.data(), order.size() * sizeof(unsigned), hipMemcpyHostToDevice));
-    c.runCount = unsigned(runs.size());
-    c.orderKey = key;
+    c.runCount = unsigned(c.runCosts.size());
+    c.orderFrames = frames;
     return true;
 }
 
+// The hybrid node layout (bvh_builder.h hybrid_bvh4) for `top` top-of-tree nodes: built on the
+// host once per (scene, top) and uploaded to the context's device.
 bool ensure_hybrid(Ctx &c, int top, const char **err) {
     State &s = S();
     SceneHost &sc = s.scene;
@@ -904,11 +915,11 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.refBits = ldsScene && wide ? packed_ref_bits(numNodes, numTris) : 0u;
                         p.rngTable = nullptr;
                         p.poolWords = poolWords;
-                        // Scene-hitting pixel runs first, the sky's last, per XCD queue (megakernel;
-                        // item_order.h).  Automatic for LDS-resident scenes (Cornell +0.3-1.0% at
-                        // full size); trees in global memory lose ~1% with it (blob70k, r5q/r5r)
-                        if (s.pathMode == 0 && (s.itemOrder == 1 || (s.itemOrder == -1 && ldsScene))) {
-                            if (!ensure_order(c, cam, nf, err)) return false;
+                        // Pixel runs by estimated sample length, longest first, per XCD queue
+                        // (megakernel; item_order.h): Cornell +2.4%, cornell_mixed +3%, blob70k
+                        // +0.8% at full size; the slowest 1/8 Cornell share -2% (r5w)
+                        if (s.pathMode == 0 && s.itemOrder != 0) {
+                            if (!ensure_order(c, cam, nf, maxDepth, err)) return false;
                             p.runOrder = c.runOrder;
                             p.runCount = c.runCount;
                         }
