@@ -896,19 +896,24 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.numMats = numMats;
                         p.ldsScene = ldsScene ? 1 : 0;
                         p.full = s.scene.full ? 1 : 0;
-                        // shade once fewer than this many lanes still traverse: LDS scenes' short node
-                        // visits favour a later exit (Cornell 16: +1.4% over 32), global-memory
-                        // trees an earlier one (blob70k 24: -3%)
-                        p.waveThreshold = s.waveThreshold >= 0 ? s.waveThreshold : ldsScene ? 16 : 32;
+                        // shade once fewer than this many lanes still traverse (re-swept in round 3
+                        // under the sample-length item order, r5y-r6a: LDS scenes 24 with the exits
+                        // below, Cornell 48.4 -> 53.7 G; global-memory trees 32, blob70k 24 and 40
+                        // lower)
+                        p.waveThreshold = s.waveThreshold >= 0 ? s.waveThreshold : ldsScene ? 24 : 32;
                         p.chunk = s.chunk;
                         // Loop exits of the traversal round (measured): trees in global
                         // memory leave the node loop once <= 17 lanes still search for a leaf (r2
                         // sweep of the 4-wide kernels: blob70k, 21 levels, best at 17-18; blob64x34
-                        // and random_scene, 16 and 12 levels, best at 15 — the round-1 rule
-                        // levels-6 gave 10 and 6, -3.7% and -1.6%), LDS scenes at 4; every scene
-                        // leaves the leaf loop once <= 48 lanes hold a leaf (Cornell 28.4 -> 31.3 G).
-                        p.leafExit = unsigned(s.leafExit >= 0 ? s.leafExit : ldsScene ? 4 : 17);
-                        p.nodeExit = unsigned(s.nodeExit >= 0 ? s.nodeExit : 48);
+                        // and random_scene, 16 and 12 levels, best at 15) and the leaf loop once
+                        // <= 48 lanes hold a leaf; LDS scenes at 12 and 8 (round 3, with the item
+                        // order: node exit 4-16 x leaf exit 8-16 within 0.6% of the best, Cornell
+                        // 53.8 G; the round-2 values 4 and 48 gave 48.4 G), except that the general
+                        // kernel and the wavefront keep leaf exit 4 (cornell_mixed +1.4%, Cornell
+                        // wavefront +6% over 12; r6b)
+                        const bool lambertMega = s.pathMode == 0 && !s.scene.full;
+                        p.leafExit = unsigned(s.leafExit >= 0 ? s.leafExit : ldsScene ? (lambertMega ? 12 : 4) : 17);
+                        p.nodeExit = unsigned(s.nodeExit >= 0 ? s.nodeExit : ldsScene ? 8 : 48);
                         p.wide = fmt;
                         p.stackCap = stackCap;
                         p.topBytes = topBytes;
