@@ -900,7 +900,10 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         // under the sample-length item order, r5y-r6a: LDS scenes 24 with the exits
                         // below, Cornell 48.4 -> 53.7 G; global-memory trees 32, blob70k 24 and 40
                         // lower)
-                        p.waveThreshold = s.waveThreshold >= 0 ? s.waveThreshold : ldsScene ? 24 : 32;
+                        // (the general megakernel over a tree in global memory: 24, random_scene
+                        // +5.8% over 32 with the exits below, r6c)
+                        const bool fullMega = s.pathMode == 0 && s.scene.full;
+                        p.waveThreshold = s.waveThreshold >= 0 ? s.waveThreshold : ldsScene || fullMega ? 24 : 32;
                         p.chunk = s.chunk;
                         // Loop exits of the traversal round (measured): trees in global
                         // memory leave the node loop once <= 17 lanes still search for a leaf (r2
@@ -911,9 +914,14 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         // 53.8 G; the round-2 values 4 and 48 gave 48.4 G), except that the general
                         // kernel and the wavefront keep leaf exit 4 (cornell_mixed +1.4%, Cornell
                         // wavefront +6% over 12; r6b)
+                        // The general megakernel over a tree in global memory: 12 and 16 (random_scene,
+                        // r6c).
                         const bool lambertMega = s.pathMode == 0 && !s.scene.full;
-                        p.leafExit = unsigned(s.leafExit >= 0 ? s.leafExit : ldsScene ? (lambertMega ? 12 : 4) : 17);
-                        p.nodeExit = unsigned(s.nodeExit >= 0 ? s.nodeExit : ldsScene ? 8 : 48);
+                        p.leafExit = unsigned(s.leafExit >= 0 ? s.leafExit
+                                              : ldsScene          ? (lambertMega ? 12 : 4)
+                                              : fullMega          ? 12
+                                                                  : 17);
+                        p.nodeExit = unsigned(s.nodeExit >= 0 ? s.nodeExit : ldsScene ? 8 : fullMega ? 16 : 48);
                         p.wide = fmt;
                         p.stackCap = stackCap;
                         p.topBytes = topBytes;
