@@ -179,7 +179,7 @@ __global__ __launch_bounds__(256) void sphere4_kernel(Sphere4Params P) {
 #ifdef HIPPT_DEBUG_TIMELINE
 // per wave: [0] start, [1] first drained fetch, [2] end (s_memrealtime, 100 MHz), [3] items,
 // [4] HW_ID, [5] XCC_ID
-__device__ unsigned long long g_timeline[65536 * 6];
+__device__ unsigned long long g_timeline[65536 * 8];
 #endif
 
 // SGPR budget.  A wave's SGPR allocation (granule 16) plus the 16 the trap handler reserves
@@ -277,11 +277,11 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     static_assert(!QUANT || (WIDE && !LDS_SCENE), "quantized nodes: 4-wide global-memory traversal only");
 #ifdef HIPPT_DEBUG_TIMELINE
     const unsigned tlw = blockIdx.x * 4u + (threadIdx.x >> 6);
-    unsigned long long tlDrained = 0, tlItems = 0;
+    unsigned long long tlDrained = 0, tlItems = 0, tlRounds = 0, tlLate = 0;
     if (__lane_id() == 0 && tlw < 65536) {
-        g_timeline[6 * tlw] = __builtin_amdgcn_s_memrealtime();
-        g_timeline[6 * tlw + 4] = __builtin_amdgcn_s_getreg(0xF804);  // HW_REG_HW_ID
-        g_timeline[6 * tlw + 5] = __builtin_amdgcn_s_getreg(0xF814);  // HW_REG_XCC_ID
+        g_timeline[8 * tlw] = __builtin_amdgcn_s_memrealtime();
+        g_timeline[8 * tlw + 4] = __builtin_amdgcn_s_getreg(0xF804);  // HW_REG_HW_ID
+        g_timeline[8 * tlw + 5] = __builtin_amdgcn_s_getreg(0xF814);  // HW_REG_XCC_ID
     }
 #endif
     // Per-lane traversal stack, P.stackDepth (= BVH interior levels) entries per lane, sized
@@ -379,6 +379,9 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         while (combLeft) combLeft = combine_chunk(P);
     for (;;) {
         prof<STATS>(pc, 0);
+#ifdef HIPPT_DEBUG_TIMELINE
+        if (tlDrained) ++tlRounds;
+#endif
         // ---- refill: every lane whose sample ended takes the next (pixel, frame) -------------
         if (POOL) {
             const unsigned long long m = __ballot(need);
@@ -516,6 +519,9 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
             if (finished) {
                 store_radiance(P.scratch, item, Lr, Lg, Lb);
                 ++samples;
+#ifdef HIPPT_DEBUG_TIMELINE
+                if (tlDrained) ++tlLate;
+#endif
                 item = kNone;
                 need = true;
             }
@@ -526,9 +532,11 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
 
 #ifdef HIPPT_DEBUG_TIMELINE
     if (__lane_id() == 0 && tlw < 65536) {
-        g_timeline[6 * tlw + 1] = tlDrained;
-        g_timeline[6 * tlw + 2] = __builtin_amdgcn_s_memrealtime();
-        g_timeline[6 * tlw + 3] = tlItems;
+        g_timeline[8 * tlw + 1] = tlDrained;
+        g_timeline[8 * tlw + 2] = __builtin_amdgcn_s_memrealtime();
+        g_timeline[8 * tlw + 3] = tlItems;
+        g_timeline[8 * tlw + 6] = tlRounds;  // loop iterations after the wave saw the queues drained
+        g_timeline[8 * tlw + 7] = tlLate;    // samples lane 0 finished after that
     }
 #endif
     const unsigned long long segsW = wave_sum(segs), samplesW = wave_sum(samples);
@@ -591,7 +599,7 @@ hipError_t launch_rng_table(uint32_t *table, hipStream_t s) {
 #ifdef HIPPT_DEBUG_TIMELINE
 extern "C" int hipptDebugTimeline(unsigned long long *out, int maxWaves) {
     const int n = maxWaves < 65536 ? maxWaves : 65536;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_timeline), size_t(n) * 6 * sizeof(unsigned long long)) == hipSuccess
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_timeline), size_t(n) * 8 * sizeof(unsigned long long)) == hipSuccess
                ? n
                : -1;
 }

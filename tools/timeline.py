@@ -42,7 +42,7 @@ def main():
     kernel_ms = pt.stats()["traceMs"]
     fn = pt._lib.hipptDebugTimeline
     fn.restype = ctypes.c_int
-    buf = np.zeros((65536, 6), np.uint64)
+    buf = np.zeros((65536, 8), np.uint64)
     n = fn(buf.ctypes.data_as(ctypes.POINTER(ctypes.c_ulonglong)), 65536)
     t = buf[:n]
     t = t[t[:, 0] > 0]
@@ -53,7 +53,10 @@ def main():
     print(json.dumps({"scene": a.scene, "chunk": a.chunk, "stride": a.stride, "spp": a.spp, "waves": int(len(t)), "kernel_ms": round(kernel_ms, 3),
                       "start_us_q": q(us(t[:, 0])), "drained_us_q": q(us(drained)), "end_us_q": q(us(t[:, 2])),
                       "end_minus_drained_us_q": q((t[:, 2].astype(np.float64) - t[:, 1]) / 100.0),
-                      "items_q": q(t[:, 3].astype(np.float64))}))
+                      "items_q": q(t[:, 3].astype(np.float64)),
+                      "rounds_after_drain_q": q(t[:, 6].astype(np.float64)),
+                      "lane_samples_after_drain_q": q(t[:, 7].astype(np.float64)),
+                      "round_us_after_drain_q": q((t[:, 2].astype(np.float64) - t[:, 1]) / 100.0 / np.maximum(1, t[:, 6]))}))
     hw = t[:, 4].astype(np.int64)
     xcc = t[:, 5].astype(np.int64) & 0xF
     cu = (hw >> 8) & 0xF
