@@ -226,7 +226,8 @@ enum {
     , HIPPT_OPT_CAMERA_POOL = 26    /* megakernel over a 4-wide float-node tree: each wave generates the camera
                                        rays of its next 64 samples with all lanes at once into an LDS pool
                                        instead of one by one as paths end (1), or not (0); -1 (default):
-                                       automatic (on for LDS-resident scenes).  Same results either way */
+                                       automatic (on except for the general kernel over a tree in global
+                                       memory).  Same results either way */
     , HIPPT_OPT_FUSE_COMBINE = 27   /* megakernel: a batch's running average + tonemap runs inside the next
                                        batch's launch on the same device (beside its paths) instead of as a
                                        launch of its own, whenever nothing reads the image in between (1), or

@@ -813,10 +813,15 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 // leaves beside the stack (automatic), or HIPPT_OPT_LDS_TOP_NODES nodes.  The
                 // wavefront keeps its 8-bit nodes (blob70k: 8.28 G 8-bit, 7.53 G float, r2za).
                 // Camera-ray pool (megakernel, 4-wide float nodes): on by default for LDS-resident
-                // scenes; a tree in global memory gives its spare LDS to the top of the tree instead.
+                // scenes and for the Lambertian kernel over a tree in global memory (its pool's LDS
+                // comes out of the top of the tree).
                 // Pinhole cameras at a nonzero origin start every ray at cam.origin exactly
                 // (origin + 0*offset), so their pool entries carry no origin.
-                const bool pool = s.pathMode == 0 && wide && !quant && (s.cameraPool == 1 || (s.cameraPool == -1 && ldsScene));
+                // (round 3, r6j: also for the Lambertian kernel over a tree in global memory,
+                // blob70k +1.8% though the pool's LDS comes out of the top; the general kernel
+                // there loses 10%, random_scene)
+                const bool pool = s.pathMode == 0 && wide && !quant &&
+                                  (s.cameraPool == 1 || (s.cameraPool == -1 && (ldsScene || !s.scene.full)));
                 if (hybrid) quant = false;  // (pool: off, as for 8-bit nodes)
                 const bool pinhole = cam.lens_radius == 0.0f && cam.origin[0] != 0.0f && cam.origin[1] != 0.0f &&
                                      cam.origin[2] != 0.0f;
