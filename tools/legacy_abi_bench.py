@@ -83,10 +83,14 @@ def main():
     ap.add_argument("--frames", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--scenes", nargs="*", default=["sphere4", "cornell34"])
+    ap.add_argument("--opt", action="append", default=[], help="KEY=VALUE hipptSetOption pair (numeric key)")
     a = ap.parse_args()
     lib = hippt.load_library()
     pt = hippt.PathTracer()
     pt.setDevices([0])
+    for o in a.opt:
+        k, v = o.split("=")
+        assert lib.hipptSetOption(int(k), int(v)), o
     out = []
     for sc in a.scenes:
         for mode in ("legacy", "present"):
