@@ -294,9 +294,10 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     // Trees in global memory (4-wide): the top of the tree (P.topBytes of the node array) at LDS
     // address 0, then the stack.
     constexpr bool TOP = WIDE && !LDS_SCENE;
-    // packed child keys: the Lambertian kernel over LDS-resident 4-wide trees (Cornell +0.8%; the
-    // general kernel lost 4.3% with them, cornell_mixed, round 3 A/B)
-    constexpr bool PACKED = WIDE && LDS_SCENE && !FULL && bool(HIPPT_PACKED_KEYS);
+    // packed child keys over LDS-resident 4-wide trees (Cornell +0.8%; the general kernel lost
+    // 4.3% with them under the round-2 loop exits and gains 0.6% under the current ones,
+    // cornell_mixed, round 3 A/Bs)
+    constexpr bool PACKED = WIDE && LDS_SCENE && bool(HIPPT_PACKED_KEYS);
     int *const stk = LDS_SCENE ? lds + P.numNodes * ldsNodeF4 * 4 : lds + (TOP ? (P.topBytes >> 2) : 0u);
     int *const my = stk + threadIdx.x;
 
