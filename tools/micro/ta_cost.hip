@@ -1,11 +1,13 @@
 // ta_cost.hip — vector-memory address-unit (TA) cost of global loads on gfx950 (experiment):
 // L2-resident buffer, many independent loads per lane; per-lane addresses scattered (each lane
 // its own 64-B line), coalesced (consecutive lanes consecutive elements) or wave-uniform.
-// Prints cycles per wave-load instruction per CU at the measured rate.
+// Prints cycles per wave-load instruction per CU at the measured rate.  ACTIVE: lanes that take
+// part (the others are masked off around the load), to see whether the TA's cost follows the
+// exec mask or the instruction.
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
-template <typename T, int PATTERN>
+template <typename T, int PATTERN, int ACTIVE = 64>
 __global__ __launch_bounds__(256) void k(const T *buf, unsigned mask, float *out, int iters) {
     float acc = 0.0f;
     const unsigned lane = threadIdx.x & 63u;
@@ -18,14 +20,16 @@ __global__ __launch_bounds__(256) void k(const T *buf, unsigned mask, float *out
             if (PATTERN == 0) e = (step + lane * 67u) & mask;        // scattered: one line per lane (64 B stride units)
             else if (PATTERN == 1) e = (step * 64u + lane) & mask;   // coalesced
             else e = step & mask;                                     // uniform
-            const T v = buf[e];
-            acc += *reinterpret_cast<const float *>(&v);
+            if (ACTIVE == 64 || lane < unsigned(ACTIVE)) {
+                const T v = buf[e];
+                acc += *reinterpret_cast<const float *>(&v);
+            }
         }
     }
     out[blockIdx.x * 256 + threadIdx.x] = acc;
 }
 
-template <typename T, int P>
+template <typename T, int P, int A = 64>
 void run(const char *name, void *buf, unsigned elems, float *out, int cus, double ghz) {
     const int blocks = cus * 8, iters = 512;
     hipEvent_t a, b;
@@ -34,7 +38,7 @@ void run(const char *name, void *buf, unsigned elems, float *out, int cus, doubl
     float ms = 0;
     for (int rep = 0; rep < 3; ++rep) {
         (void)hipEventRecord(a);
-        k<T, P><<<blocks, 256>>>((const T *)buf, elems - 1, out, iters);
+        k<T, P, A><<<blocks, 256>>>((const T *)buf, elems - 1, out, iters);
         (void)hipEventRecord(b);
         (void)hipEventSynchronize(b);
         (void)hipEventElapsedTime(&ms, a, b);
@@ -61,6 +65,9 @@ int main() {
     run<float4, 0>("dwordx4 scattered", buf, bytes / 16, out, cus, ghz);
     run<float, 1>("dword coalesced", buf, bytes / 4, out, cus, ghz);
     run<float4, 1>("dwordx4 coalesced", buf, bytes / 16, out, cus, ghz);
+    run<float4, 0, 32>("dwordx4 scattered 32", buf, bytes / 16, out, cus, ghz);
+    run<float4, 0, 16>("dwordx4 scattered 16", buf, bytes / 16, out, cus, ghz);
+    run<float4, 0, 4>("dwordx4 scattered 4", buf, bytes / 16, out, cus, ghz);
     run<float, 2>("dword uniform", buf, bytes / 4, out, cus, ghz);
     run<float4, 2>("dwordx4 uniform", buf, bytes / 16, out, cus, ghz);
     return 0;
