@@ -205,8 +205,10 @@ enum {
                                        whose bound exceeds 19, the rest of the LDS holding the top
                                        of the tree) */
     , HIPPT_OPT_BVH_QUANT = 19      /* 4-wide traversal of global-memory trees over 64-byte nodes with 8-bit
-                                       child boxes (1) or 128-byte float nodes (0); -1 (default): 8-bit for
-                                       the wavefront path's Lambertian-triangle scenes */
+                                       child boxes (1) or 128-byte float nodes (0); 2: float top in LDS,
+                                       8-bit nodes below (megakernel); 3: 128-byte nodes of half-precision
+                                       planes, 4 reads per visit (megakernel); -1 (default): 8-bit for
+                                       the wavefront path's Lambertian-triangle scenes, else float */
     , HIPPT_OPT_LDS_TOP_NODES = 20  /* 4-wide traversal of global-memory trees: the top of the tree (this many
                                        nodes, breadth-first) is copied into every block's LDS and read from
                                        there; 0: none; -1 (default): automatic (what the LDS budget of the

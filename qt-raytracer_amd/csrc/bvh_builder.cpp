@@ -733,4 +733,54 @@ bool hybrid_bvh4(const Bvh4 &b, const std::vector<uint32_t> &q, int topNodes, st
     return true;
 }
 
+float half_value(uint16_t h) {
+    const int e = (h >> 10) & 31, m = h & 1023;
+    const double mag = e == 31 ? (m ? NAN : INFINITY) : e == 0 ? std::ldexp(double(m), -24)
+                                                               : std::ldexp(double(1024 + m), e - 25);
+    return float((h & 0x8000u) ? -mag : mag);
+}
+
+// |x| truncated to a half (toward zero; finite values beyond the largest half give it), as bits
+static uint16_t half_trunc_mag(double a) {
+    if (std::isinf(a)) return 0x7C00u;
+    if (a >= 65504.0) return 0x7BFFu;
+    if (a < std::ldexp(1.0, -14)) return uint16_t(std::floor(std::ldexp(a, 24)));  // subnormal / zero
+    int e = 0;
+    const double f = std::frexp(a, &e);  // a = f * 2^e, f in [0.5, 1)
+    const int m = int(std::floor(std::ldexp(f, 11))) - 1024;
+    return uint16_t(((e + 14) << 10) | m);
+}
+
+uint16_t half_round_down(float x) {
+    const double a = std::fabs(double(x));
+    uint16_t h = half_trunc_mag(a);
+    if (std::signbit(x)) {
+        if (half_value(h) != float(a)) ++h;  // truncation rounded a negative value up: one step away
+        h |= 0x8000u;
+    }
+    return h;
+}
+
+uint16_t half_round_up(float x) { return uint16_t(half_round_down(-x) ^ 0x8000u); }
+
+void half_bvh4(const uint32_t *in, size_t numNodes, std::vector<uint32_t> &out) {
+    out.assign(numNodes * kNode4Words, 0u);
+    for (size_t k = 0; k < numNodes; ++k) {
+        const uint32_t *w = in + k * kNode4Words;
+        uint16_t *h = reinterpret_cast<uint16_t *>(out.data() + k * kNode4Words);
+        for (int a = 0; a < 3; ++a)
+            for (int i = 0; i < 4; ++i) {
+                float lo, hi;
+                std::memcpy(&lo, w + 8 * a + i, 4);
+                std::memcpy(&hi, w + 8 * a + 4 + i, 4);
+                const uint16_t l = half_round_down(lo), u = half_round_up(hi);
+                h[16 * a + i] = l;  // [lo hi]: positive direction
+                h[16 * a + 4 + i] = u;
+                h[16 * a + 8 + i] = u;  // [hi lo]: negative direction
+                h[16 * a + 12 + i] = l;
+            }
+        std::memcpy(out.data() + k * kNode4Words + 24, w + 24, 16);  // codes at byte 96
+    }
+}
+
 }  // namespace hippt

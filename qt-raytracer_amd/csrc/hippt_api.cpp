@@ -84,6 +84,7 @@ struct Ctx {
     float4 *nodes4 = nullptr;  // 4-wide BVH (same primitive order as nodes)
     float4 *nodes4q = nullptr; // the 4-wide BVH with 8-bit child boxes
     float4 *nodes4h = nullptr; // hybrid layout (float top + 8-bit nodes) for hybridTop top nodes
+    float4 *nodes4f = nullptr; // the 4-wide BVH with half-precision planes (half_bvh4)
     int hybridTop = -1;
     // the queues' pixel-run order of this context's rows (HIPPT_OPT_ITEM_ORDER), built per key
     unsigned *runOrder = nullptr;
@@ -122,6 +123,7 @@ struct SceneHost {
     int numTris = 0, numNodes = 0, levels = 0;  // numTris: primitive records (triangles + spheres)
     std::vector<float4> nodes4;                 // 4-wide BVH (bvh_builder.h Bvh4)
     std::vector<float4> nodes4q;                // quantize_bvh4 of it
+    std::vector<float4> nodes4f;                // half_bvh4 of it (device codes)
     hippt::Bvh4 bvh4;                           // the 4-wide tree with node-index codes ...
     std::vector<uint32_t> q4;                   // ... and its 8-bit nodes (hybrid_bvh4 inputs)
     std::vector<float4> hybrid;                 // hybrid_bvh4 for hybridTop top nodes (built on use)
@@ -268,7 +270,8 @@ void free_scene_buffers(Ctx &c) {
     (void)hipFree(c.nodes4);
     (void)hipFree(c.nodes4q);
     (void)hipFree(c.nodes4h);
-    c.nodes = c.tris = c.shade = c.mats = c.nodes4 = c.nodes4q = c.nodes4h = nullptr;
+    (void)hipFree(c.nodes4f);
+    c.nodes = c.tris = c.shade = c.mats = c.nodes4 = c.nodes4q = c.nodes4h = c.nodes4f = nullptr;
     c.hybridTop = -1;
     (void)hipFree(c.runOrder);
     c.runOrder = nullptr;
@@ -383,7 +386,8 @@ bool ensure_scene(Ctx &c, const char **err) {
         return true;
     };
     if (!up(c.nodes, s.scene.nodes) || !up(c.tris, s.scene.tris) || !up(c.shade, s.scene.shade) ||
-        !up(c.mats, s.scene.mats) || !up(c.nodes4, s.scene.nodes4) || !up(c.nodes4q, s.scene.nodes4q))
+        !up(c.mats, s.scene.mats) || !up(c.nodes4, s.scene.nodes4) || !up(c.nodes4q, s.scene.nodes4q) ||
+        !up(c.nodes4f, s.scene.nodes4f))
         return false;
     c.sceneVersion = s.scene.version;
     return true;
@@ -807,7 +811,11 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 bool hybrid = wide && !ldsScene && !s.scene.nodes4q.empty() && s.pathMode == 0 && s.bvhQuant == 2 &&
                               s.ldsTopNodes != 0;
                 bool quant = wide && !ldsScene && !s.scene.nodes4q.empty() &&
-                             (s.bvhQuant >= 1 || (s.bvhQuant == -1 && !s.scene.full && s.pathMode == 1));
+                             (s.bvhQuant == 1 || s.bvhQuant == 2 ||
+                              (s.bvhQuant == -1 && !s.scene.full && s.pathMode == 1));
+                // Half-precision planes (HIPPT_OPT_BVH_QUANT 3, megakernel): the float nodes' size and
+                // codes, 4 reads per visit instead of 7 (the wavefront keeps its default)
+                const bool half = wide && !ldsScene && s.pathMode == 0 && s.bvhQuant == 3;
                 // The top of a global-memory tree in LDS (megakernel and wavefront extend): the
                 // breadth-first prefix of the node array that the LDS budget of the resident blocks
                 // leaves beside the stack (automatic), or HIPPT_OPT_LDS_TOP_NODES nodes.  The
@@ -843,12 +851,16 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                     hybrid = false;
                     quant = true;
                 }
-                const int fmt = !wide ? hippt::kWide2 : hybrid ? hippt::kWideHybrid : quant ? hippt::kWideQuant
-                                                                                      : hippt::kWideFloat;
+                const int fmt = !wide    ? hippt::kWide2
+                                : hybrid ? hippt::kWideHybrid
+                                : quant  ? hippt::kWideQuant
+                                : half   ? hippt::kWideHalf
+                                         : hippt::kWideFloat;
                 if (hybrid && !ensure_hybrid(c, int(topBytes / 128), err)) return false;
                 const long long occKey =
                     occupancy_key(s.scene.version, stackDepth, ldsScene, s.scene.full, wide, quant, spills) ^
-                    ((long long)topBytes << 40) ^ ((long long)poolWords << 36) ^ ((long long)hybrid << 35);
+                    ((long long)topBytes << 40) ^ ((long long)poolWords << 36) ^ ((long long)hybrid << 35) ^
+                    ((long long)half << 34);
                 if (c.occKey != occKey) {
                     const int ln = ldsScene ? numNodes : 0, lt = ldsScene ? numTris : 0, lm = ldsScene ? numMats : 0;
                     c.meshBlocksPerCu[0] = hippt::mesh_blocks_per_cu(false, s.scene.full, fmt, stackDepth, ln, lt,
@@ -873,7 +885,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         HIP_TRY(hipMemsetAsync(scratch, 0, size_t(total) * 3 * sizeof(float), c.stream));
                     } else {
                         hippt::MeshParams p{};
-                        p.nodes = hybrid ? c.nodes4h : quant ? c.nodes4q : wide ? c.nodes4 : c.nodes;
+                        p.nodes = hybrid ? c.nodes4h : quant ? c.nodes4q : half ? c.nodes4f : wide ? c.nodes4 : c.nodes;
                         p.tris = c.tris;
                         p.shade = c.shade;
                         p.mats = c.mats;
@@ -1157,6 +1169,12 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
     };
     byte_codes(sc.nodes4, hippt::kNode4Words, 24, hippt::kNode4Words * 4);
     byte_codes(sc.nodes4q, hippt::kNode4QWords, 12, hippt::kNode4QWords * 4);
+    {
+        std::vector<uint32_t> h;
+        hippt::half_bvh4(reinterpret_cast<const uint32_t *>(sc.nodes4.data()), size_t(sc.numNodes4), h);
+        sc.nodes4f.assign(h.size() / 4, float4{});
+        std::memcpy(sc.nodes4f.data(), h.data(), h.size() * sizeof(uint32_t));
+    }
     sc.levels4 = bvh4.levels;
     sc.stackBound4 = bvh4.stackBound;
     sc.tris.assign(size_t(numPrims) * 3, float4{});
@@ -1541,7 +1559,7 @@ extern "C" bool hipptSetOption(int key, long long value) {
         s.stackCap = int(value);
         return true;
     case HIPPT_OPT_BVH_QUANT:
-        if (value < -1 || value > 2) return false;
+        if (value < -1 || value > 3) return false;
         s.bvhQuant = int(value);
         return true;
     case HIPPT_OPT_LDS_TOP_NODES:

@@ -69,7 +69,8 @@ struct MeshParams {
     unsigned nodeExit;     // leaf loop exits once <= nodeExit lanes still hold a leaf (0: never)
     // Node format (kWide*): 0 the 2-wide tree; 1 the 4-wide tree (Bvh4 layout, 8 float4 per node);
     // 2 quantize_bvh4 layout (4 float4 per node; global-memory scenes only); 3 hybrid_bvh4 (the
-    // top's topBytes as float nodes, read from LDS, then 8-bit nodes; global-memory scenes only).
+    // top's topBytes as float nodes, read from LDS, then 8-bit nodes; global-memory scenes only);
+    // 4 half_bvh4 (128-byte nodes of half-precision planes, the Bvh4 codes; global-memory scenes).
     // LDS stack content capacity and the per-lane spill area (spillCap entries per lane of the
     // persistent grid; null if never used)
     int wide;
@@ -104,7 +105,7 @@ struct MeshParams {
 
 
 // MeshParams::wide
-enum { kWide2 = 0, kWideFloat = 1, kWideQuant = 2, kWideHybrid = 3 };
+enum { kWide2 = 0, kWideFloat = 1, kWideQuant = 2, kWideHybrid = 3, kWideHalf = 4 };
 
 // Material kinds (RayTracer.h:473-540) and the sphere flag of a shading record.
 enum { kLambertian = 0, kMetal = 1, kDielectric = 2 };

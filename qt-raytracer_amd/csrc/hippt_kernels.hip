@@ -272,7 +272,7 @@ __device__ __forceinline__ void pool_take(const MeshParams &P, const float *pool
 }
 
 template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE, bool QUANT, bool SPILL = true, bool POOL = false,
-          bool HYBRID = false>
+          bool HYBRID = false, bool HALF = false>
 __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_EU : HIPPT_MESH_WAVES_PER_EU) HIPPT_SGPR_ATTR void mesh_kernel(MeshParams P) {
     static_assert(!QUANT || (WIDE && !LDS_SCENE), "quantized nodes: 4-wide global-memory traversal only");
 #ifdef HIPPT_DEBUG_TIMELINE
@@ -465,7 +465,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         if (!CAP || __any(busy(T))) do {
             prof<STATS>(pc, 2);
             if (WIDE)
-                traverse_round_wide<nodeF4, STATS, FULL, QUANT, SPILL, LDS_SCENE, TOP, HYBRID, PACKED>(
+                traverse_round_wide<nodeF4, STATS, FULL, QUANT, SPILL, LDS_SCENE, TOP, HYBRID, PACKED, HALF>(
                     T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit, S, P.topBytes, P.refBits);
             else
                 traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
@@ -634,7 +634,7 @@ size_t mesh_lds_block_budget() { return (size_t(160u << 10) / kMaxResidentBlocks
 
 using MeshFn = void (*)(MeshParams);
 // node formats (MeshParams::wide): 2-wide, 4-wide float, 4-wide quantized, 4-wide hybrid (float
-// top in LDS, quantized below it); the quantized formats are for global-memory trees only
+// top in LDS, quantized below it), 4-wide half planes; the last three are for global-memory trees only
 // 4-wide trees whose stack bound fits the LDS capacity run a variant without the spill/refill
 // code (timed builds; the counting builds keep one variant, the results are the same)
 // (the camera-ray pool: 4-wide float-node kernels)
@@ -642,6 +642,7 @@ template <bool STATS, bool FULL, bool SPILL, bool POOL>
 static MeshFn mesh_fn_wide(bool lds, int fmt) {
     if (lds) return mesh_kernel<STATS, true, FULL, true, false, SPILL, POOL>;
     if (fmt == kWideHybrid) return mesh_kernel<STATS, false, FULL, true, true, SPILL, false, true>;
+    if (fmt == kWideHalf) return mesh_kernel<STATS, false, FULL, true, false, SPILL, POOL, false, true>;
     return fmt == kWideQuant ? mesh_kernel<STATS, false, FULL, true, true, SPILL>
                              : mesh_kernel<STATS, false, FULL, true, false, SPILL, POOL>;
 }
@@ -662,7 +663,7 @@ hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hip
     if (p.stackDepth < 1 || p.stackDepth > kStackDepth) return hipErrorInvalidValue;
     if (p.wide && (p.stackCap < 1 || p.stackCap + 2 > p.stackDepth)) return hipErrorInvalidValue;
     const bool lds = p.ldsScene != 0;
-    if (p.wide < kWide2 || p.wide > kWideHybrid || (lds && p.wide >= kWideQuant)) return hipErrorInvalidValue;
+    if (p.wide < kWide2 || p.wide > kWideHalf || (lds && p.wide >= kWideQuant)) return hipErrorInvalidValue;
     // the top of the tree: whole nodes of the LDS-read format (8-bit nodes only for kWideQuant)
     if (p.topBytes && (lds || p.wide == kWide2 || p.topBytes % (p.wide == kWideQuant ? 64u : 128u) ||
                        p.topBytes > (unsigned(p.numNodes) << (p.wide == kWideQuant ? 6 : 7))))
@@ -670,7 +671,7 @@ hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hip
     if (p.wide == kWideHybrid && !p.topBytes) return hipErrorInvalidValue;  // hybrid trees start in LDS
     if (lds && p.wide == kWideFloat && (p.refBits < 8 || p.refBits > 20)) return hipErrorInvalidValue;
     const bool pool = p.poolWords != 0;
-    if (pool && (p.wide != kWideFloat || (p.poolWords != kPoolWordsPinhole && p.poolWords != kPoolWordsFull)))
+    if (pool && ((p.wide != kWideFloat && p.wide != kWideHalf) || (p.poolWords != kPoolWordsPinhole && p.poolWords != kPoolWordsFull)))
         return hipErrorInvalidValue;
     const size_t bytes = mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0, p.wide != 0, p.topBytes,
                                         lds ? p.numMats : 0, p.poolWords);

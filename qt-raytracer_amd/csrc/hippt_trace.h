@@ -786,6 +786,13 @@ __device__ __forceinline__ float4 lds_ld4(unsigned a) {
     return make_float4(v.x, v.y, v.z, v.w);
 }
 
+// The four children's planes of a half_bvh4 (near, far) read: halves 0-3 near, 4-7 far.  The
+// conversions fold into the slab test's FMAs (v_fma_mix_f32 with op_sel).
+__device__ __forceinline__ float hlo(unsigned w) { return float(__builtin_bit_cast(_Float16, (unsigned short)(w & 0xffffu))); }
+__device__ __forceinline__ float hhi(unsigned w) { return float(__builtin_bit_cast(_Float16, (unsigned short)(w >> 16))); }
+__device__ __forceinline__ float4 half_near(uint4 w) { return make_float4(hlo(w.x), hhi(w.x), hlo(w.y), hhi(w.y)); }
+__device__ __forceinline__ float4 half_far(uint4 w) { return make_float4(hlo(w.z), hhi(w.z), hlo(w.w), hhi(w.w)); }
+
 // Compare-exchange of (key, child code) pairs: afterwards ka <= kb.
 __device__ __forceinline__ void cas(unsigned &ka, int &ca, unsigned &kb, int &cb) {
     const bool sw = kb < ka;
@@ -838,8 +845,11 @@ __device__ __forceinline__ void cas_key(unsigned &ka, unsigned &kb) {
 // which then run both paths (blob70k 17.5 vs 20.9 G); visiting the top first, the lanes below it
 // waiting, was worse still (11.7 G).
 // PACKED (LDS-resident scenes): packed child keys (pack_key), refBits low bits carrying the code.
+// HALF (with TOP, trees in global memory; bvh_builder.h half_bvh4): the same 128-byte nodes with
+// half-precision planes, each axis's near and far planes one aligned 16-byte read (4 reads per
+// visit instead of 7 where the TA binds), the slab FMAs taking the halves directly (v_fma_mix_f32).
 template <int NODE_F4, bool STATS, bool FULL, bool QUANT = false, bool SPILL = true, bool LDS0 = false,
-          bool TOP = false, bool HYBRID = false, bool PACKED = false>
+          bool TOP = false, bool HYBRID = false, bool PACKED = false, bool HALF = false>
 __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *my, const float4 *nodes,
                                                     const float4 *tris, unsigned long long &nvis,
                                                     unsigned long long &ntest, unsigned *pc, unsigned leafExit,
@@ -847,6 +857,7 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
                                                     unsigned topBytes = 0, unsigned refBits = 0) {
     static_assert(!HYBRID || (QUANT && TOP), "hybrid trees: 8-bit nodes below an LDS top");
     static_assert(!PACKED || (LDS0 && !QUANT), "packed keys: LDS-resident float trees");
+    static_assert(!HALF || (TOP && !QUANT && !LDS0), "half planes: 4-wide trees in global memory");
     const unsigned refMask = PACKED ? (1u << refBits) - 1u : 0u;
     const float tmin = 0.001f;
     // near-row byte offsets of this ray's octant within a node (x at 0/16, y at 32/48, z at 64/80)
@@ -866,7 +877,29 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
             const unsigned ax = nb | sx, ay = nb | sy, az = nb | sz;
             // LDS0: the nodes are the LDS scene copy at LDS address 0
             float4 nx, fx, ny, fy, nz, fz, cw;
-            if (LDS0 || HYBRID || topVisit) {
+            if (HALF) {
+                // the octant's (near, far) row of each axis: the float node's near-row address
+                float4 vx, vy, vz;
+                if (topVisit) {
+                    vx = lds_ld4(nb | sx);
+                    vy = lds_ld4(nb | sy);
+                    vz = lds_ld4(nb | sz);
+                    cw = lds_ld4(nb + 96u);
+                } else {
+                    vx = ld4(nodes, nb | sx);
+                    vy = ld4(nodes, nb | sy);
+                    vz = ld4(nodes, nb | sz);
+                    cw = ld4(nodes, nb + 96u);
+                }
+                const uint4 wx = *reinterpret_cast<const uint4 *>(&vx), wy = *reinterpret_cast<const uint4 *>(&vy),
+                            wz = *reinterpret_cast<const uint4 *>(&vz);
+                nx = half_near(wx);
+                fx = half_far(wx);
+                ny = half_near(wy);
+                fy = half_far(wy);
+                nz = half_near(wz);
+                fz = half_far(wz);
+            } else if (LDS0 || HYBRID || topVisit) {
                 nx = lds_ld4(ax);
                 fx = lds_ld4(ax ^ 16u);
                 ny = lds_ld4(ay);

@@ -1,6 +1,6 @@
 """Seeded random scenes (GPU): triangle soups with degenerate, tiny, huge, axis-aligned and
 edge-sharing triangles, overlapping spheres, all three materials, pinhole and thin-lens cameras,
-rendered through the C ABI in the LDS-resident, global-memory (float, 8-bit and hybrid nodes),
+rendered through the C ABI in the LDS-resident, global-memory (float, 8-bit, hybrid and half-plane nodes),
 2-wide and wavefront paths, and
 compared bit for bit (ARGB words, accumulation floats, segment counts) with the oracle.
 
@@ -79,6 +79,7 @@ MODES = {
     "wide2": ((hippt.OPT_LDS_SCENE, 0), (hippt.OPT_BVH_WIDTH, 2), (hippt.OPT_PATH_MODE, 0)),
     "quant8": ((hippt.OPT_LDS_SCENE, 0), (hippt.OPT_BVH_WIDTH, 0), (hippt.OPT_BVH_QUANT, 1)),
     "hybrid": ((hippt.OPT_LDS_SCENE, 0), (hippt.OPT_BVH_WIDTH, 0), (hippt.OPT_BVH_QUANT, 2)),
+    "half": ((hippt.OPT_LDS_SCENE, 0), (hippt.OPT_BVH_WIDTH, 0), (hippt.OPT_BVH_QUANT, 3)),
     "wavefront": ((hippt.OPT_LDS_SCENE, 1), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_PATH_MODE, 1),
                   (hippt.OPT_WAVEFRONT_SLOTS, 500)),
 }

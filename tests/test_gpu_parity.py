@@ -310,7 +310,8 @@ def test_bvh_width_and_stack_spill_do_not_change_results(pt, name):
     ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
     for lds in (1, 0):
         pt.setOption(hippt.OPT_LDS_SCENE, lds)
-        for width, cap, quant in ((2, 0, -1), (0, 0, -1), (4, 0, 0), (4, 0, 1), (4, 4, 1), (4, 7, 0)):
+        for width, cap, quant in ((2, 0, -1), (0, 0, -1), (4, 0, 0), (4, 0, 1), (4, 4, 1), (4, 7, 0), (4, 0, 3),
+                                  (4, 4, 3)):
             pt.setOption(hippt.OPT_BVH_WIDTH, width)
             pt.setOption(hippt.OPT_STACK_CAP, cap)
             pt.setOption(hippt.OPT_BVH_QUANT, quant)
@@ -333,8 +334,9 @@ def test_lds_top_of_tree_does_not_change_results(pt, name):
     pt.setOption(hippt.OPT_LDS_SCENE, 0)
     w, h = (40, 24) if name == "random_scene" else (56, 40)
     ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
-    # 0 float nodes, 1 8-bit nodes (top too), 2 hybrid: float top in LDS, 8-bit nodes below
-    quants = (0, 2) if name == "random_scene" else (0, 1, 2)
+    # 0 float nodes, 1 8-bit nodes (top too), 2 hybrid: float top in LDS, 8-bit nodes below,
+    # 3 half-precision planes (top too)
+    quants = (0, 2, 3) if name == "random_scene" else (0, 1, 2, 3)
     for quant in quants:
         for cap in (0, 4):
             for top in (0, 1, 5, 85, -1):
