@@ -114,6 +114,9 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=8.0, help="target duration of one CPU sample run")
     p.add_argument("--cpu-runs", type=int, default=3, help="CPU sample runs (the median is reported)")
     p.add_argument("--cpu-threads", type=int, default=None)
+    p.add_argument("--option", action="append", default=[], metavar="NAME=V",
+                   help="any library option by its hippt.h name without HIPPT_OPT_ (e.g. BVH_QUANT=3); "
+                        "recorded in config.options")
     p.add_argument("--pmc", default=None, help="PMC summary JSON for roofline.traffic")
     a = p.parse_args()
     if a.preset:
@@ -340,6 +343,17 @@ def main():
     pt.setOption(hippt.OPT_PATH_MODE, 1 if args.path_mode == "wavefront" else 0)
     if args.wavefront_slots is not None:
         pt.setOption(hippt.OPT_WAVEFRONT_SLOTS, args.wavefront_slots)
+    options = {}
+    for kv in args.option:
+        name, _, v = kv.partition("=")
+        key = getattr(hippt, "OPT_" + name.upper(), None)
+        if key is None or not v.lstrip("-").isdigit():
+            raise SystemExit(f"--option {kv}: unknown option")
+        try:
+            pt.setOption(key, int(v))
+        except hippt.HipptError as e:
+            raise SystemExit(f"--option {kv}: {e}") from None
+        options[name.upper()] = int(v)
     pt.uploadMesh(scene)
     if not pt.initialize(args.width, args.height):
         raise SystemExit(pt.lastError())
@@ -445,6 +459,7 @@ def main():
                 "wave_threshold": pt._lib.hipptGetOption(hippt.OPT_WAVE_THRESHOLD),
                 "chunk": pt._lib.hipptGetOption(hippt.OPT_CHUNK),
                 "image_crc32": zlib.crc32(full.tobytes()) & 0xFFFFFFFF,
+                **({"options": options} if options else {}),
             },
             "roofline": roofline,
             "cpu_baseline": cpu,
