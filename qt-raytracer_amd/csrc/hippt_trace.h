@@ -881,14 +881,14 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
                 // the octant's (near, far) row of each axis: the float node's near-row address
                 float4 vx, vy, vz;
                 if (topVisit) {
-                    vx = lds_ld4(nb | sx);
-                    vy = lds_ld4(nb | sy);
-                    vz = lds_ld4(nb | sz);
+                    vx = lds_ld4(ax);
+                    vy = lds_ld4(ay);
+                    vz = lds_ld4(az);
                     cw = lds_ld4(nb + 96u);
                 } else {
-                    vx = ld4(nodes, nb | sx);
-                    vy = ld4(nodes, nb | sy);
-                    vz = ld4(nodes, nb | sz);
+                    vx = ld4(nodes, ax);
+                    vy = ld4(nodes, ay);
+                    vz = ld4(nodes, az);
                     cw = ld4(nodes, nb + 96u);
                 }
                 const uint4 wx = *reinterpret_cast<const uint4 *>(&vx), wy = *reinterpret_cast<const uint4 *>(&vy),

@@ -56,6 +56,26 @@ def test_legacy_abi_frames_match_oracle(pt, w, h):
     _assert_same(px, acc, ora_px, ora_acc)
 
 
+@pytest.mark.parametrize("w,h,share", [(320, 240, None), (512, 256, (1, 2)), (1920, 1080, None)])
+def test_legacy_large_frames_match_oracle(pt, w, h, share):
+    """Blocking frames at the app's size (1920x1080) and at an interleaved row share: the host
+    pixels the call hands out and the accumulation are the oracle's, frame after frame."""
+    if share:
+        pt.setRowInterleave(*share)
+    assert pt.initialize(w, h), pt.lastError()
+    frames = 2 if w == 1920 else 3
+    for _ in range(frames):
+        assert pt.renderFrame(8), pt.lastError()
+    px = pt.hostPixels()
+    _, acc = pt.readback()
+    ora_px, ora_acc = po.sphere4(w, h, 0, frames, 8)
+    if share:
+        r, n = share
+        _assert_same(px[r::n], acc[r::n], ora_px[r::n], ora_acc[r::n])
+    else:
+        _assert_same(px, acc, ora_px, ora_acc)
+
+
 def test_legacy_reinit_resets_accumulation(pt):
     # RayTracerFboItem.cpp:520-521 calls initialize again on frame 0
     assert pt.initialize(32, 16)
