@@ -61,6 +61,11 @@ struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
 };
 
+#ifndef HIPPT_LEGACY_ZERO_COPY
+#define HIPPT_LEGACY_ZERO_COPY 1
+#endif
+constexpr bool kLegacyZeroCopy = HIPPT_LEGACY_ZERO_COPY != 0;
+
 struct Ctx {
     int device = 0;
     int y0 = 0, rows = 0, stride = 1;  // image rows y0, y0+stride, ... (rows of them)
@@ -520,7 +525,10 @@ bool init_inner(int width, int height, const char **err) {
         HIP_TRY(hipStreamSynchronize(c.stream));
     }
     s.hostCount = size_t(width) * size_t(height);
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.host), s.hostCount * sizeof(unsigned), hipHostMallocPortable));
+    // portable, mapped, coherent (fine-grained: the GPU writes go straight to host memory): every
+    // context's device may write it (legacy zero-copy frames)
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.host), s.hostCount * sizeof(unsigned),
+                          hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent));
     std::memset(s.host, 0, s.hostCount * sizeof(unsigned));
     s.ready = true;
     return true;
@@ -720,6 +728,7 @@ bool flush_deferred(Ctx &c, const char **err) {
     HIP_TRY(hippt::launch_combine(c.deferred, c.stream));
     HIP_TRY(hipEventRecord(ev.b, c.stream));
     c.pending.push_back({1, ev});
+    c.deferred.hostOut = nullptr;
     return true;
 }
 
@@ -750,12 +759,22 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
         HIP_TRY(hipSetDevice(c.device));
         const int rows = c.rows;
         const unsigned bandPixels = unsigned(rows) * unsigned(s.width);
+        bool copied = false;  // the kernel wrote the frame's rows into s.host (legacy zero copy)
         if (rows > 0 && count > 0) {
             if (!mesh) {
                 // the legacy kernel writes accum/out itself: a mesh batch's pending combine goes first
                 if (!flush_deferred(c, err)) return false;
                 hippt::Sphere4Params p{c.accum, c.out, c.stats, s.width, s.height, c.y0, rows, c.stride, firstFrame, count,
-                                       maxDepth, s.pixelFormat};
+                                       maxDepth, s.pixelFormat, nullptr};
+                // A blocking frame (the app's cudaPathTracerRender): the kernel writes the words into
+                // the pinned host frame itself, overlapping the PCIe transfer with the trace, instead
+                // of a D2H copy after it (1080p: 0.17 ms of copy behind 0.13 ms of kernel)
+                if (copy && kLegacyZeroCopy) {
+                    void *d = nullptr;
+                    HIP_TRY(hipHostGetDevicePointer(&d, s.host, 0));
+                    p.hostOut = static_cast<uint32_t *>(d);
+                    copied = true;
+                }
                 EventPair ev;
                 if (!next_events(c, ev, err)) return false;
                 HIP_TRY(hipEventRecord(ev.a, c.stream));
@@ -985,8 +1004,18 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 }
             }
         }
+        if (copy && rows > 0 && c.hasDeferred && kLegacyZeroCopy) {
+            // a blocking mesh frame: its combine writes the words into the pinned host frame too
+            void *d = nullptr;
+            HIP_TRY(hipHostGetDevicePointer(&d, s.host, 0));
+            c.deferred.hostOut = static_cast<uint32_t *>(d);
+            c.deferred.width = s.width;
+            c.deferred.y0 = c.y0;
+            c.deferred.stride = c.stride;
+            copied = true;
+        }
         if (copy && !flush_deferred(c, err)) return false;
-        if (copy && rows > 0) {
+        if (copy && rows > 0 && !copied) {
             if (!copy_rows_async(c, s.host, c.out, sizeof(uint32_t), err)) return false;
         }
     }

@@ -22,6 +22,7 @@ struct Sphere4Params {
     int width, height, y0, rows, rowStride;  // image rows y0 + k*rowStride, k < rows
     int firstFrame, frames, maxDepth;
     int format;  // kPixelArgb / kPixelRgba8
+    uint32_t *hostOut;  // null, or the W*H full frame in pinned host memory (device-mapped)
 };
 
 // Pixel word formats of the output frame (HIPPT_OPT_PIXEL_FORMAT)
@@ -36,6 +37,10 @@ struct CombineParams {
     unsigned bandPixels, totalItems;
     int firstFrame, frames;
     int format;  // kPixelArgb / kPixelRgba8
+    // combine_kernel only (a blocking frame): the words also into the pinned full W*H host frame
+    // (device-mapped), band pixel p at row y0 + (p / width) * stride; null: device words only
+    uint32_t *hostOut;
+    int width, y0, stride;
 };
 
 // Mesh megakernel: one persistent grid drains `totalItems` (pixel, frame) samples of the band's

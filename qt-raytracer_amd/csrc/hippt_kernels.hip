@@ -156,6 +156,9 @@ __global__ __launch_bounds__(256) void sphere4_kernel(Sphere4Params P) {
         if (P.frames > 0) {
             P.accum[idx] = acc;
             P.out[idx] = outp;
+            // a blocking frame's word also straight into the caller's pinned frame (full-frame
+            // row y): the PCIe writes stream out while other waves still trace
+            if (P.hostOut) P.hostOut[size_t(y) * size_t(P.width) + size_t(x)] = outp;
         }
     }
     segs = wave_sum(segs);
@@ -211,7 +214,7 @@ __device__ unsigned long long g_timeline[65536 * 8];
 #endif
 // Running average in frame order, then the output word (CudaPathTracerKernel.cu:157-178), of band
 // pixel p over a batch of per-sample radiances.
-template <int UNROLL>
+template <int UNROLL, bool HOST = false>
 __device__ __forceinline__ void combine_pixel(const CombineParams &P, unsigned p) {
     float4 acc = P.accum[p];
 #pragma unroll UNROLL
@@ -226,7 +229,12 @@ __device__ __forceinline__ void combine_pixel(const CombineParams &P, unsigned p
     }
     acc.w = 1.0f;
     P.accum[p] = acc;
-    P.out[p] = pack_pixel(acc.x, acc.y, acc.z, P.format);
+    const uint32_t word = pack_pixel(acc.x, acc.y, acc.z, P.format);
+    P.out[p] = word;
+    if (HOST && P.hostOut) {
+        const unsigned yb = p / unsigned(P.width), x = p - yb * unsigned(P.width);
+        P.hostOut[size_t(unsigned(P.y0) + yb * unsigned(P.stride)) * unsigned(P.width) + x] = word;
+    }
 }
 
 // One 64-pixel chunk of the previous batch's combine (MeshParams::comb) for the whole wave; false
@@ -566,7 +574,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
 // Running average in frame order, then ARGB (CudaPathTracerKernel.cu:157-178).
 __global__ __launch_bounds__(256) void combine_kernel(CombineParams P) {
     const unsigned stride = gridDim.x * 256u;
-    for (unsigned p = blockIdx.x * 256u + threadIdx.x; p < P.bandPixels; p += stride) combine_pixel<8>(P, p);
+    for (unsigned p = blockIdx.x * 256u + threadIdx.x; p < P.bandPixels; p += stride) combine_pixel<8, true>(P, p);
 }
 
 // table[s] for s = 0 .. 2^32-1: the state from which random_in_unit_sphere, entered with state s,
