@@ -81,6 +81,7 @@ struct Ctx {
     float *scratchAlt = nullptr;
     size_t scratchAltBytes = 0;
     hippt::CombineParams deferred{};
+    hippt::HostFrame deferredHost{};  // a blocking frame's flush: the words into the host frame too
     bool hasDeferred = false;
     unsigned *queue = nullptr;
     unsigned long long *stats = nullptr;
@@ -725,10 +726,10 @@ bool flush_deferred(Ctx &c, const char **err) {
     EventPair ev;
     if (!next_events(c, ev, err)) return false;
     HIP_TRY(hipEventRecord(ev.a, c.stream));
-    HIP_TRY(hippt::launch_combine(c.deferred, c.stream));
+    HIP_TRY(hippt::launch_combine(c.deferred, c.stream, c.deferredHost));
     HIP_TRY(hipEventRecord(ev.b, c.stream));
     c.pending.push_back({1, ev});
-    c.deferred.hostOut = nullptr;
+    c.deferredHost = hippt::HostFrame{};
     return true;
 }
 
@@ -1008,10 +1009,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
             // a blocking mesh frame: its combine writes the words into the pinned host frame too
             void *d = nullptr;
             HIP_TRY(hipHostGetDevicePointer(&d, s.host, 0));
-            c.deferred.hostOut = static_cast<uint32_t *>(d);
-            c.deferred.width = s.width;
-            c.deferred.y0 = c.y0;
-            c.deferred.stride = c.stride;
+            c.deferredHost = hippt::HostFrame{static_cast<uint32_t *>(d), s.width, c.y0, c.stride};
             copied = true;
         }
         if (copy && !flush_deferred(c, err)) return false;

@@ -37,9 +37,12 @@ struct CombineParams {
     unsigned bandPixels, totalItems;
     int firstFrame, frames;
     int format;  // kPixelArgb / kPixelRgba8
-    // combine_kernel only (a blocking frame): the words also into the pinned full W*H host frame
-    // (device-mapped), band pixel p at row y0 + (p / width) * stride; null: device words only
-    uint32_t *hostOut;
+};
+
+// combine_kernel's output words also into the pinned full W*H host frame (device-mapped; a
+// blocking frame), band pixel p at row y0 + (p / width) * stride; host null: device words only
+struct HostFrame {
+    uint32_t *host;
     int width, y0, stride;
 };
 
@@ -127,7 +130,7 @@ inline hipError_t check_lds_at_zero(const void *kernel) {
 
 hipError_t launch_sphere4(const Sphere4Params &p, hipStream_t s);
 hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hipStream_t s);
-hipError_t launch_combine(const CombineParams &p, hipStream_t s);
+hipError_t launch_combine(const CombineParams &p, hipStream_t s, const HostFrame &h = HostFrame{});
 // random_in_unit_sphere's rejection loop (RayTracer.h:155-161 with the hash RNG and the short-cycle
 // escape) is a pure function of the RNG state it starts from: table[s] = the state from which the
 // accepted candidate's three draws are made.  One 32-bit word per state: 16 GiB.

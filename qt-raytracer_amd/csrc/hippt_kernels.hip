@@ -215,7 +215,7 @@ __device__ unsigned long long g_timeline[65536 * 8];
 // Running average in frame order, then the output word (CudaPathTracerKernel.cu:157-178), of band
 // pixel p over a batch of per-sample radiances.
 template <int UNROLL, bool HOST = false>
-__device__ __forceinline__ void combine_pixel(const CombineParams &P, unsigned p) {
+__device__ __forceinline__ void combine_pixel(const CombineParams &P, unsigned p, const HostFrame &H = HostFrame{}) {
     float4 acc = P.accum[p];
 #pragma unroll UNROLL
     for (int fl = 0; fl < P.frames; ++fl) {
@@ -231,9 +231,9 @@ __device__ __forceinline__ void combine_pixel(const CombineParams &P, unsigned p
     P.accum[p] = acc;
     const uint32_t word = pack_pixel(acc.x, acc.y, acc.z, P.format);
     P.out[p] = word;
-    if (HOST && P.hostOut) {
-        const unsigned yb = p / unsigned(P.width), x = p - yb * unsigned(P.width);
-        P.hostOut[size_t(unsigned(P.y0) + yb * unsigned(P.stride)) * unsigned(P.width) + x] = word;
+    if (HOST && H.host) {
+        const unsigned yb = p / unsigned(H.width), x = p - yb * unsigned(H.width);
+        H.host[size_t(unsigned(H.y0) + yb * unsigned(H.stride)) * unsigned(H.width) + x] = word;
     }
 }
 
@@ -572,9 +572,9 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
 }
 
 // Running average in frame order, then ARGB (CudaPathTracerKernel.cu:157-178).
-__global__ __launch_bounds__(256) void combine_kernel(CombineParams P) {
+__global__ __launch_bounds__(256) void combine_kernel(CombineParams P, HostFrame H) {
     const unsigned stride = gridDim.x * 256u;
-    for (unsigned p = blockIdx.x * 256u + threadIdx.x; p < P.bandPixels; p += stride) combine_pixel<8, true>(P, p);
+    for (unsigned p = blockIdx.x * 256u + threadIdx.x; p < P.bandPixels; p += stride) combine_pixel<8, true>(P, p, H);
 }
 
 // table[s] for s = 0 .. 2^32-1: the state from which random_in_unit_sphere, entered with state s,
@@ -693,11 +693,11 @@ hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hip
     return hipGetLastError();
 }
 
-hipError_t launch_combine(const CombineParams &p, hipStream_t s) {
+hipError_t launch_combine(const CombineParams &p, hipStream_t s, const HostFrame &h) {
     if (p.bandPixels == 0) return hipSuccess;
     unsigned blocks = (p.bandPixels + 255u) / 256u;
     if (blocks > 8192u) blocks = 8192u;
-    hipLaunchKernelGGL(combine_kernel, dim3(blocks), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(combine_kernel, dim3(blocks), dim3(256), 0, s, p, h);
     return hipGetLastError();
 }
 
