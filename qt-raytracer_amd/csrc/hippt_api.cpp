@@ -750,8 +750,11 @@ bool batch_scratch(Ctx &c, size_t need, float **out, const char **err) {
     return true;
 }
 
-bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const char **err) {
+// copy: the frame's words end in the full-frame pinned host buffer `dst` (State::host when null),
+// written by the kernel that makes them (legacy kernel or combine) or copied after it.
+bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const char **err, unsigned *dst = nullptr) {
     State &s = S();
+    if (!dst) dst = s.host;
     if (!s.ready) return fail(err, "HIP path tracer not initialized");
     if (count < 0) return fail(err, "negative frame count");
     const bool mesh = s.scene.kind == HIPPT_SCENE_MESH;
@@ -772,7 +775,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 // of a D2H copy after it (1080p: 0.17 ms of copy behind 0.13 ms of kernel)
                 if (copy && kLegacyZeroCopy) {
                     void *d = nullptr;
-                    HIP_TRY(hipHostGetDevicePointer(&d, s.host, 0));
+                    HIP_TRY(hipHostGetDevicePointer(&d, dst, 0));
                     p.hostOut = static_cast<uint32_t *>(d);
                     copied = true;
                 }
@@ -1008,13 +1011,13 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
         if (copy && rows > 0 && c.hasDeferred && kLegacyZeroCopy) {
             // a blocking mesh frame: its combine writes the words into the pinned host frame too
             void *d = nullptr;
-            HIP_TRY(hipHostGetDevicePointer(&d, s.host, 0));
+            HIP_TRY(hipHostGetDevicePointer(&d, dst, 0));
             c.deferredHost = hippt::HostFrame{static_cast<uint32_t *>(d), s.width, c.y0, c.stride};
             copied = true;
         }
         if (copy && !flush_deferred(c, err)) return false;
         if (copy && rows > 0 && !copied) {
-            if (!copy_rows_async(c, s.host, c.out, sizeof(uint32_t), err)) return false;
+            if (!copy_rows_async(c, dst, c.out, sizeof(uint32_t), err)) return false;
         }
     }
     return true;
@@ -1377,16 +1380,16 @@ extern "C" bool hipptSynchronize(const char **err) {
 extern "C" bool hipptRenderFramesPresent(int firstFrame, int count, int maxDepth, const char **err) {
     std::lock_guard<std::mutex> g(S().mu);
     State &s = S();
-    if (!enqueue_locked(firstFrame, count, maxDepth, false, err)) return false;
+    if (!s.ready) return fail(err, "HIP path tracer not initialized");
     const int b = s.presentNext;
+    // mapped + coherent like State::host: the frame's kernel writes the hand-off frame itself
     if (!s.present[b])
         HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&s.present[b]), s.hostCount * sizeof(unsigned),
-                              hipHostMallocPortable));
+                              hipHostMallocPortable | hipHostMallocMapped | hipHostMallocCoherent));
+    if (!enqueue_locked(firstFrame, count, maxDepth, true, err, s.present[b])) return false;
     for (Ctx &c : s.ctxs) {
-        if (!flush_deferred(c, err)) return false;
         HIP_TRY(hipSetDevice(c.device));
         if (!c.presentEv[b]) HIP_TRY(hipEventCreateWithFlags(&c.presentEv[b], hipEventDisableTiming));
-        if (!copy_rows_async(c, s.present[b], c.out, sizeof(uint32_t), err)) return false;
         HIP_TRY(hipEventRecord(c.presentEv[b], c.stream));
         if (!harvest_locked(c, err)) return false;
     }
