@@ -139,10 +139,11 @@ bool hipptRenderFrames(int firstFrame, int count, int maxDepth, const unsigned i
 bool hipptRenderFramesAsync(int firstFrame, int count, int maxDepth, const char **errorMessage);
 bool hipptSynchronize(const char **errorMessage);
 /* Interactive hand-off (replaces the blocking full-frame copy of CudaPathTracerKernel.cu:261-265
- * for hosts that can show the previous image): enqueues the frames and a copy of the ARGB image
- * into one of two library-owned pinned frames, and returns without waiting. */
+ * for hosts that can show the previous image): enqueues the frames, whose ARGB image lands in one
+ * of two library-owned pinned frames (written by the kernel that produces it, or copied after
+ * it), and returns without waiting. */
 bool hipptRenderFramesPresent(int firstFrame, int count, int maxDepth, const char **errorMessage);
-/* Never blocks: *hostPixels = the newest presented image whose copy has completed (null if
+/* Never blocks: *hostPixels = the newest presented image whose transfer has completed (null if
  * none yet), *frames = the frame count accumulated in it.  The image stays valid until the
  * second hipptRenderFramesPresent call after the one that produced it (double buffering). */
 bool hipptLatestFrame(const unsigned int **hostPixels, int *frames, const char **errorMessage);
