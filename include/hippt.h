@@ -208,7 +208,7 @@ enum {
     , HIPPT_OPT_BVH_QUANT = 19      /* 4-wide traversal of global-memory trees over 64-byte nodes with 8-bit
                                        child boxes (1) or 128-byte float nodes (0); 2: float top in LDS,
                                        8-bit nodes below (megakernel); 3: 128-byte nodes of half-precision
-                                       planes, 4 reads per visit (megakernel); -1 (default): 8-bit for
+                                       planes, 4 reads per visit (megakernel and wavefront); -1 (default): 8-bit for
                                        the wavefront path's Lambertian-triangle scenes, else float */
     , HIPPT_OPT_LDS_TOP_NODES = 20  /* 4-wide traversal of global-memory trees: the top of the tree (this many
                                        nodes, breadth-first) is copied into every block's LDS and read from

@@ -640,7 +640,7 @@ bool run_wavefront(Ctx &c, hippt::MeshParams p, bool cnt, bool spills, int spill
     W.hit = reinterpret_cast<float2 *>(base + 6 * entries);
     const bool wide = p.wide != 0, quant = p.wide == 2;
     const long long occKey = occupancy_key(s.scene.version, p.stackDepth, p.ldsScene != 0, p.full != 0, wide, quant) ^
-                             ((long long)p.topBytes << 40);
+                             ((long long)p.topBytes << 40) ^ ((long long)(p.wide == hippt::kWideHalf) << 34);
     if (c.wfOccKey != occKey) {
         const int ln = p.ldsScene ? p.numNodes : 0, lt = p.ldsScene ? p.numTris : 0;
         c.wfBlocksPerCu[0] =
@@ -836,9 +836,9 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 bool quant = wide && !ldsScene && !s.scene.nodes4q.empty() &&
                              (s.bvhQuant == 1 || s.bvhQuant == 2 ||
                               (s.bvhQuant == -1 && !s.scene.full && s.pathMode == 1));
-                // Half-precision planes (HIPPT_OPT_BVH_QUANT 3, megakernel): the float nodes' size and
-                // codes, 4 reads per visit instead of 7 (the wavefront keeps its default)
-                const bool half = wide && !ldsScene && s.pathMode == 0 && s.bvhQuant == 3;
+                // Half-precision planes (HIPPT_OPT_BVH_QUANT 3, megakernel and wavefront extend): the
+                // float nodes' size and codes, 4 reads per visit instead of 7
+                const bool half = wide && !ldsScene && s.bvhQuant == 3;
                 // The top of a global-memory tree in LDS (megakernel and wavefront extend): the
                 // breadth-first prefix of the node array that the LDS budget of the resident blocks
                 // leaves beside the stack (automatic), or HIPPT_OPT_LDS_TOP_NODES nodes.  The

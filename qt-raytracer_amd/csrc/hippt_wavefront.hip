@@ -80,8 +80,9 @@ __global__ void wf_init(WfParams W) {
     if (i < unsigned(kCtrCount)) W.ctr[ctr_word(int(i))] = 0;
 }
 
-// WIDE: the megakernel's 4-wide traversal (QUANT: over 8-bit child boxes, global memory only).
-template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE, bool QUANT>
+// WIDE: the megakernel's 4-wide traversal (QUANT: over 8-bit child boxes, HALF: over half-precision
+// planes; global memory only).
+template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE, bool QUANT, bool HALF = false>
 __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
     extern __shared__ int lds[];  // LDS scene: nodes at address 0, then stack, primitives
     constexpr int ldsNodeF4 = WIDE ? kLdsNode4F4 : kLdsNodeF4;  // mesh_lds_bytes layout
@@ -168,7 +169,7 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
         if (!__any(busy(T))) break;
         do {
             if (WIDE)
-                traverse_round_wide<nodeF4, STATS, FULL, QUANT, true, LDS_SCENE, TOP>(
+                traverse_round_wide<nodeF4, STATS, FULL, QUANT, true, LDS_SCENE, TOP, false, false, HALF>(
                     T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit, S, P.topBytes);
             else
                 traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
@@ -276,14 +277,16 @@ __global__ __launch_bounds__(kWfBlock) void wf_generate(WfParams W, int nxt) {
 
 using ExtFn = void (*)(WfParams, int);
 template <bool STATS, bool FULL>
-ExtFn ext_fn_fmt(bool lds, bool wide, bool quant) {
+ExtFn ext_fn_fmt(bool lds, bool wide, bool quant, bool half) {
     if (lds) return wide ? wf_extend<STATS, true, FULL, true, false> : wf_extend<STATS, true, FULL, false, false>;
     if (!wide) return wf_extend<STATS, false, FULL, false, false>;
+    if (half) return wf_extend<STATS, false, FULL, true, false, true>;
     return quant ? wf_extend<STATS, false, FULL, true, true> : wf_extend<STATS, false, FULL, true, false>;
 }
-ExtFn ext_fn(bool count, bool lds, bool full, bool wide, bool quant) {
-    if (count) return full ? ext_fn_fmt<true, true>(lds, wide, quant) : ext_fn_fmt<true, false>(lds, wide, quant);
-    return full ? ext_fn_fmt<false, true>(lds, wide, quant) : ext_fn_fmt<false, false>(lds, wide, quant);
+ExtFn ext_fn(bool count, bool lds, bool full, bool wide, bool quant, bool half = false) {
+    if (count)
+        return full ? ext_fn_fmt<true, true>(lds, wide, quant, half) : ext_fn_fmt<true, false>(lds, wide, quant, half);
+    return full ? ext_fn_fmt<false, true>(lds, wide, quant, half) : ext_fn_fmt<false, false>(lds, wide, quant, half);
 }
 
 }  // namespace
@@ -316,7 +319,8 @@ hipError_t wf_launch_extend(const WfParams &W, int cur, int blocks, bool countTr
                        P.topBytes > (unsigned(P.numNodes) << (P.wide == 2 ? 6 : 7))))
         return hipErrorInvalidValue;
     const size_t bytes = mesh_lds_bytes(P.stackDepth, lds ? P.numNodes : 0, lds ? P.numTris : 0, P.wide != 0, P.topBytes);
-    const auto fn = ext_fn(countTraversal, lds, P.full != 0, P.wide != 0, P.wide == 2 && !lds);
+    const auto fn = ext_fn(countTraversal, lds, P.full != 0, P.wide != 0, P.wide == kWideQuant && !lds,
+                           P.wide == kWideHalf && !lds);
     if (P.wide && (lds || P.topBytes)) {  // the variant launched (8-bit nodes included) reads LDS at 0
         const hipError_t e = check_lds_at_zero(reinterpret_cast<const void *>(fn));
         if (e != hipSuccess) return e;

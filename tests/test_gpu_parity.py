@@ -156,6 +156,28 @@ def test_wavefront_matches_oracle(pt, name, w, h, spp, depth, slots, width, cap)
     assert st["segments"] == segs and st["pixelSamples"] == samples
 
 
+@pytest.mark.parametrize("name", ["blob70k", "random_scene"])
+@pytest.mark.parametrize("quant", [0, 1, 3])
+def test_wavefront_node_formats_match_oracle(pt, name, quant):
+    """The wavefront's extend kernel over a tree in global memory with float, 8-bit and
+    half-precision nodes (HIPPT_OPT_BVH_QUANT 0 / 1 / 3), the top of each in LDS: the oracle's image,
+    segment and sample counts."""
+    sc = scenes.get_scene(name)
+    pt.uploadMesh(sc)
+    pt.setOption(hippt.OPT_LDS_SCENE, 0)
+    pt.setOption(hippt.OPT_PATH_MODE, 1)
+    pt.setOption(hippt.OPT_BVH_QUANT, quant)
+    w, h = (40, 24) if name == "random_scene" else (56, 40)
+    assert pt.initialize(w, h), pt.lastError()
+    pt.resetStats()
+    assert pt.renderFrames(3, 8), pt.lastError()
+    px, acc = pt.readback()
+    ora_px, ora_acc, segs, samples = po.MeshScene(sc, w, h).frames(0, 3, 8)
+    _assert_same(px, acc, ora_px, ora_acc)
+    st = pt.stats()
+    assert st["segments"] == segs and st["pixelSamples"] == samples
+
+
 @pytest.mark.parametrize("slots", [1 << 21, 1 << 24])
 def test_wavefront_equals_megakernel_1080p(pt, slots):
     """Full-width frames; 2^21 slots regenerate (shards refill unevenly), 2^24 hold every path."""
