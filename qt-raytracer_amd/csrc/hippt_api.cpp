@@ -90,7 +90,8 @@ struct Ctx {
     float4 *nodes4 = nullptr;  // 4-wide BVH (same primitive order as nodes)
     float4 *nodes4q = nullptr; // the 4-wide BVH with 8-bit child boxes
     float4 *nodes4h = nullptr; // hybrid layout (float top + 8-bit nodes) for hybridTop top nodes
-    float4 *nodes4f = nullptr; // the 4-wide BVH with half-precision planes (half_bvh4)
+    float4 *nodes4f = nullptr; // the 4-wide BVH with half-precision planes (half_bvh4; on use)
+    int halfVersion = -1;      // scene version of nodes4f
     int hybridTop = -1;
     // the queues' pixel-run order of this context's rows (HIPPT_OPT_ITEM_ORDER), built per key
     unsigned *runOrder = nullptr;
@@ -129,7 +130,7 @@ struct SceneHost {
     int numTris = 0, numNodes = 0, levels = 0;  // numTris: primitive records (triangles + spheres)
     std::vector<float4> nodes4;                 // 4-wide BVH (bvh_builder.h Bvh4)
     std::vector<float4> nodes4q;                // quantize_bvh4 of it
-    std::vector<float4> nodes4f;                // half_bvh4 of it (device codes)
+    std::vector<float4> nodes4f;                // half_bvh4 of it (device codes; built on use)
     hippt::Bvh4 bvh4;                           // the 4-wide tree with node-index codes ...
     std::vector<uint32_t> q4;                   // ... and its 8-bit nodes (hybrid_bvh4 inputs)
     std::vector<float4> hybrid;                 // hybrid_bvh4 for hybridTop top nodes (built on use)
@@ -278,6 +279,7 @@ void free_scene_buffers(Ctx &c) {
     (void)hipFree(c.nodes4h);
     (void)hipFree(c.nodes4f);
     c.nodes = c.tris = c.shade = c.mats = c.nodes4 = c.nodes4q = c.nodes4h = c.nodes4f = nullptr;
+    c.halfVersion = -1;
     c.hybridTop = -1;
     (void)hipFree(c.runOrder);
     c.runOrder = nullptr;
@@ -392,8 +394,7 @@ bool ensure_scene(Ctx &c, const char **err) {
         return true;
     };
     if (!up(c.nodes, s.scene.nodes) || !up(c.tris, s.scene.tris) || !up(c.shade, s.scene.shade) ||
-        !up(c.mats, s.scene.mats) || !up(c.nodes4, s.scene.nodes4) || !up(c.nodes4q, s.scene.nodes4q) ||
-        !up(c.nodes4f, s.scene.nodes4f))
+        !up(c.mats, s.scene.mats) || !up(c.nodes4, s.scene.nodes4) || !up(c.nodes4q, s.scene.nodes4q))
         return false;
     c.sceneVersion = s.scene.version;
     return true;
@@ -447,6 +448,27 @@ bool ensure_order(Ctx &c, const CameraF &cam, int frames, int maxDepth, const ch
         HIP_TRY(hipMemcpy(c.runOrder, order.data(), order.size() * sizeof(unsigned), hipMemcpyHostToDevice));
     c.runCount = unsigned(c.runCosts.size());
     c.orderFrames = frames;
+    return true;
+}
+
+// The half-precision node layout (bvh_builder.h half_bvh4, HIPPT_OPT_BVH_QUANT 3): built on the host
+// once per scene and uploaded to a context's device the first time a render there uses it.
+bool ensure_half(Ctx &c, const char **err) {
+    SceneHost &sc = S().scene;
+    if (sc.nodes4f.empty()) {
+        std::vector<uint32_t> h;
+        hippt::half_bvh4(reinterpret_cast<const uint32_t *>(sc.nodes4.data()), size_t(sc.numNodes4), h);
+        sc.nodes4f.assign(h.size() / 4, float4{});
+        std::memcpy(sc.nodes4f.data(), h.data(), h.size() * sizeof(uint32_t));
+    }
+    if (c.halfVersion == sc.version && c.nodes4f) return true;
+    HIP_TRY(hipSetDevice(c.device));
+    HIP_TRY(hipStreamSynchronize(c.stream));
+    (void)hipFree(c.nodes4f);
+    c.nodes4f = nullptr;
+    HIP_TRY(hipMalloc(&c.nodes4f, sc.nodes4f.size() * sizeof(float4)));
+    HIP_TRY(hipMemcpy(c.nodes4f, sc.nodes4f.data(), sc.nodes4f.size() * sizeof(float4), hipMemcpyHostToDevice));
+    c.halfVersion = sc.version;
     return true;
 }
 
@@ -880,6 +902,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                                 : half   ? hippt::kWideHalf
                                          : hippt::kWideFloat;
                 if (hybrid && !ensure_hybrid(c, int(topBytes / 128), err)) return false;
+                if (half && !ensure_half(c, err)) return false;
                 const long long occKey =
                     occupancy_key(s.scene.version, stackDepth, ldsScene, s.scene.full, wide, quant, spills) ^
                     ((long long)topBytes << 40) ^ ((long long)poolWords << 36) ^ ((long long)hybrid << 35) ^
@@ -1199,12 +1222,7 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
     };
     byte_codes(sc.nodes4, hippt::kNode4Words, 24, hippt::kNode4Words * 4);
     byte_codes(sc.nodes4q, hippt::kNode4QWords, 12, hippt::kNode4QWords * 4);
-    {
-        std::vector<uint32_t> h;
-        hippt::half_bvh4(reinterpret_cast<const uint32_t *>(sc.nodes4.data()), size_t(sc.numNodes4), h);
-        sc.nodes4f.assign(h.size() / 4, float4{});
-        std::memcpy(sc.nodes4f.data(), h.data(), h.size() * sizeof(uint32_t));
-    }
+    sc.nodes4f.clear();
     sc.levels4 = bvh4.levels;
     sc.stackBound4 = bvh4.stackBound;
     sc.tris.assign(size_t(numPrims) * 3, float4{});
