@@ -772,6 +772,17 @@ bool batch_scratch(Ctx &c, size_t need, float **out, const char **err) {
     return true;
 }
 
+// The device address of a mapped pinned host frame on the current device, or null where the
+// runtime cannot map it (the caller then copies after the kernel).
+uint32_t *host_frame_on_device(unsigned *frame) {
+    void *d = nullptr;
+    if (hipHostGetDevicePointer(&d, frame, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return static_cast<uint32_t *>(d);
+}
+
 // copy: the frame's words end in the full-frame pinned host buffer `dst` (State::host when null),
 // written by the kernel that makes them (legacy kernel or combine) or copied after it.
 bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const char **err, unsigned *dst = nullptr) {
@@ -796,10 +807,8 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 // the pinned host frame itself, overlapping the PCIe transfer with the trace, instead
                 // of a D2H copy after it (1080p: 0.17 ms of copy behind 0.13 ms of kernel)
                 if (copy && kLegacyZeroCopy) {
-                    void *d = nullptr;
-                    HIP_TRY(hipHostGetDevicePointer(&d, dst, 0));
-                    p.hostOut = static_cast<uint32_t *>(d);
-                    copied = true;
+                    p.hostOut = host_frame_on_device(dst);
+                    copied = p.hostOut != nullptr;  // else the copy after the kernel
                 }
                 EventPair ev;
                 if (!next_events(c, ev, err)) return false;
@@ -1033,10 +1042,10 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
         }
         if (copy && rows > 0 && c.hasDeferred && kLegacyZeroCopy) {
             // a blocking mesh frame: its combine writes the words into the pinned host frame too
-            void *d = nullptr;
-            HIP_TRY(hipHostGetDevicePointer(&d, dst, 0));
-            c.deferredHost = hippt::HostFrame{static_cast<uint32_t *>(d), s.width, c.y0, c.stride};
-            copied = true;
+            if (uint32_t *d = host_frame_on_device(dst)) {
+                c.deferredHost = hippt::HostFrame{d, s.width, c.y0, c.stride};
+                copied = true;
+            }
         }
         if (copy && !flush_deferred(c, err)) return false;
         if (copy && rows > 0 && !copied) {
