@@ -383,6 +383,13 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     // in 8 starts with it while the others trace, and every wave takes what is left when its
     // paths run out (the launch's tail, where the traversal leaves SIMDs idle).  Not inside the
     // path loop: with the paths' state live it costs registers.
+    // Tail finish (the camera-pool kernel over a tree in global memory): once the wave has found
+    // the queues drained, its traversal rounds run until no lane traverses (no wave-threshold
+    // exit), so its last iterations are not one node visit each: the slowest 1/8 blob70k share
+    // 3.36 -> 3.27 ms, full size unchanged; LDS scenes lose 1% on the share and keep the exit
+    // 
+    constexpr bool FINISH = POOL && !LDS_SCENE;
+    unsigned waveThr = unsigned(P.waveThreshold);
     bool combLeft = P.comb.bandPixels != 0;
     if (combLeft && (blockIdx.x & 1u) == 0 && threadIdx.x < 64u)
         while (combLeft) combLeft = combine_chunk(P);
@@ -440,6 +447,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                     depth = 0;
                     fresh = true;
                 }
+                if (FINISH && __ballot(took && item == kNone)) waveThr = 0u;
             }
         } else if (__ballot(need)) {
             const unsigned it = order_item(P, queue_fetch(need, Q, P.queue, P.totalItems, P.chunk));
@@ -477,7 +485,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                     T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit, S, P.topBytes, P.refBits);
             else
                 traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
-        } while (__popcll(__ballot(busy(T))) > unsigned(P.waveThreshold));
+        } while (__popcll(__ballot(busy(T))) > (FINISH ? waveThr : unsigned(P.waveThreshold)));
 
         // ---- shading: lanes whose traversal finished (ray_color step, RayTracer.h:579-596) ----
         if (item != kNone && !busy(T)) {
