@@ -343,6 +343,10 @@ def main():
     pt.setOption(hippt.OPT_PATH_MODE, 1 if args.path_mode == "wavefront" else 0)
     if args.wavefront_slots is not None:
         pt.setOption(hippt.OPT_WAVEFRONT_SLOTS, args.wavefront_slots)
+    # the item order's run-cost estimate on the first call (not on a host thread while the first
+    # steps run in image order, HIPPT_OPT_ITEM_ORDER's automatic mode): the timed steps are the
+    # steady state of a fixed camera either way
+    pt.setOption(hippt.OPT_ITEM_ORDER, 1)
     options = {}
     for kv in args.option:
         name, _, v = kv.partition("=")

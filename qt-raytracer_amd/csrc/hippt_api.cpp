@@ -14,11 +14,15 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <exception>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -52,10 +56,16 @@ constexpr int kSpillStackCap = 10;
 // of the node array is the top of the tree; trees read from global memory keep such a prefix in
 // LDS (HIPPT_OPT_LDS_TOP_NODES)
 constexpr int kTopOrderNodes = 1365;  // 6 complete levels
+// drain export defaults (HIPPT_OPT_DRAIN_EXPORT, HIPPT_OPT_TAIL_BLOCKS_PER_CU)
+constexpr int kDrainExportAuto = 0;
+constexpr int kTailBlocksPerCuAuto = 2;
 // hippt_trace.h kQueues x kQueueStride work counters, then (its own line) the fused combine's
 // chunk counter (MeshParams::combCtr)
 constexpr size_t kCombCtrWord = 8 * 32;
-constexpr size_t kQueueBytes = (kCombCtrWord + 32) * sizeof(unsigned);
+// then the drain export's record count and the tail launch's claim counter (MeshParams::exportCtr,
+// exportClaim), each on its own line
+constexpr size_t kExportCtrWord = kCombCtrWord + 32, kExportClaimWord = kCombCtrWord + 64;
+constexpr size_t kQueueBytes = (kCombCtrWord + 96) * sizeof(unsigned);
 
 struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
@@ -65,6 +75,35 @@ struct EventPair {
 #define HIPPT_LEGACY_ZERO_COPY 1
 #endif
 constexpr bool kLegacyZeroCopy = HIPPT_LEGACY_ZERO_COPY != 0;
+
+// The key of a context's run-cost estimates (item order): what the estimate depends on.
+struct OrderKey {
+    int version = -1, width = 0, height = 0, y0 = 0, rows = 0, stride = 0, maxDepth = 0;
+    CameraF cam{};
+};
+
+bool same_key(const OrderKey &a, const OrderKey &b) {
+    if (a.version != b.version || a.width != b.width || a.height != b.height || a.y0 != b.y0 || a.rows != b.rows ||
+        a.stride != b.stride || a.maxDepth != b.maxDepth || a.cam.lens_radius != b.cam.lens_radius)
+        return false;
+    for (int k = 0; k < 3; ++k)
+        if (a.cam.origin[k] != b.cam.origin[k] || a.cam.llc[k] != b.cam.llc[k] ||
+            a.cam.horizontal[k] != b.cam.horizontal[k] || a.cam.vertical[k] != b.cam.vertical[k] ||
+            a.cam.u[k] != b.cam.u[k] || a.cam.v[k] != b.cam.v[k])
+            return false;
+    return true;
+}
+
+// Run costs computed on a host thread of their own (HIPPT_OPT_ITEM_ORDER automatic): the thread
+// reads only the job's copies of the tree and primitives, so scene uploads and renders go on.
+struct CostJob {
+    OrderKey key;
+    hippt::Bvh4 bvh;
+    std::vector<float4> tris;
+    std::vector<float> cost;
+    std::atomic<bool> done{false};
+    std::thread th;
+};
 
 struct Ctx {
     int device = 0;
@@ -93,18 +132,28 @@ struct Ctx {
     float4 *nodes4f = nullptr; // the 4-wide BVH with half-precision planes (half_bvh4; on use)
     int halfVersion = -1;      // scene version of nodes4f
     int hybridTop = -1;
-    // the queues' pixel-run order of this context's rows (HIPPT_OPT_ITEM_ORDER), built per key
-    unsigned *runOrder = nullptr;
-    unsigned runCount = 0;
-    struct OrderKey {
-        int version = -1, width = 0, height = 0, y0 = 0, rows = 0, stride = 0, maxDepth = 0;
-        CameraF cam{};
-    } orderKey;                  // of runCosts
+    // the queues' pixel-run order of this context's rows (HIPPT_OPT_ITEM_ORDER): run costs per key,
+    // device item tables per batch size for those costs
+    OrderKey orderKey;            // of runCosts
     std::vector<float> runCosts;  // per run of 64 band pixels (item_order.h run_costs)
     bool runCostsValid = false;
-    int orderFrames = 0;          // batch size of the table in runOrder
+    struct OrderTable {
+        int frames;
+        unsigned *dev;
+    };
+    std::vector<OrderTable> orderTables;  // most recently used first, at most kOrderTables
+    struct RetiredTable {
+        unsigned *dev;
+        hipEvent_t done;  // recorded on the stream after the last launch that may read it
+    };
+    std::vector<RetiredTable> retiredTables;
+    std::shared_ptr<CostJob> costJob;  // automatic mode: the costs of a new key, off the render path
     int *spill = nullptr;      // 4-wide traversal: per-lane stack spill area
     size_t spillBytes = 0;
+    float4 *exportBuf = nullptr;  // drain export records (MeshParams::exportBuf), one per lane of the grid
+    size_t exportBytes = 0;
+    long long tailOccKey = -1;  // tail-launch occupancy cached like occKey
+    int tailBlocksPerCu = 0;
     // wavefront path-state pool (allocated on first use)
     void *wfPool = nullptr;
     unsigned wfSlots = 0;  // slots allocated
@@ -181,6 +230,8 @@ struct State {
     int cameraPool = -1;  // megakernel camera-ray pool (HIPPT_OPT_CAMERA_POOL; -1: automatic)
     int fuseCombine = -1;  // combine inside the next megakernel launch (HIPPT_OPT_FUSE_COMBINE)
     int itemOrder = -1;    // scene-hitting pixel runs first (HIPPT_OPT_ITEM_ORDER; -1: automatic)
+    int drainExport = -1;  // live-path threshold of the drain export (HIPPT_OPT_DRAIN_EXPORT; -1: automatic)
+    int tailBlocksPerCu = 0;  // the tail launch's grid (HIPPT_OPT_TAIL_BLOCKS_PER_CU; 0: automatic)
     std::vector<std::pair<int, uint32_t *>> rngTables;  // per device, built on first use
     unsigned activeTopBytes = 0;  // of the last mesh render (hipptGetOption HIPPT_INFO_*)
     int activeBlocksPerCu = 0;
@@ -208,6 +259,15 @@ bool fail(const char **errorMessage, const std::string &msg) {
     s.error[sizeof(s.error) - 1] = '\0';
     if (errorMessage) *errorMessage = s.error;
     return false;
+}
+
+// fail() for the C ABI's exception handlers (no lock held there: the entry point's lock_guard is gone
+// by the time its function-try-block's handler runs).  An exception (std::bad_alloc from a scene
+// buffer sized by caller input, ...) becomes the reference's false + message
+// (CudaPathTracerKernel.cu:181-184) instead of crossing extern "C" into std::terminate.
+bool fail_free(const char **errorMessage, const char *what) {
+    std::lock_guard<std::mutex> g(S().mu);
+    return fail(errorMessage, std::string("HIP path tracer: ") + (what ? what : "exception"));
 }
 
 #define HIP_TRY(expr)                                                                     \
@@ -269,6 +329,48 @@ void build_camera(const double lookfrom[3], const double lookat[3], const double
     out.reserved = 0.0f;
 }
 
+// Item tables no launch reads any more are freed; with `all`, after waiting for the stream.
+void free_retired_tables(Ctx &c, bool all) {
+    size_t k = 0;
+    for (auto &t : c.retiredTables) {
+        if (all || hipEventQuery(t.done) == hipSuccess) {
+            if (all) (void)hipEventSynchronize(t.done);
+            (void)hipFree(t.dev);
+            (void)hipEventDestroy(t.done);
+        } else {
+            c.retiredTables[k++] = t;
+        }
+    }
+    c.retiredTables.resize(k);
+}
+
+// A table the queued launches may still read: freed once the stream has passed this point.
+void retire_table(Ctx &c, unsigned *dev) {
+    hipEvent_t e = nullptr;
+    if (hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(e, c.stream) != hipSuccess) {
+        if (e) (void)hipEventDestroy(e);
+        (void)hipStreamSynchronize(c.stream);
+        (void)hipFree(dev);
+        return;
+    }
+    c.retiredTables.push_back({dev, e});
+}
+
+void join_cost_job(Ctx &c) {
+    if (c.costJob && c.costJob->th.joinable()) c.costJob->th.join();
+    c.costJob.reset();
+}
+
+// Forgets the run costs and every item table (scene buffers freed, context destroyed).
+void drop_order(Ctx &c) {
+    join_cost_job(c);
+    for (auto &t : c.orderTables) retire_table(c, t.dev);
+    c.orderTables.clear();
+    c.orderKey = OrderKey{};
+    c.runCostsValid = false;
+}
+
 void free_scene_buffers(Ctx &c) {
     (void)hipFree(c.nodes);
     (void)hipFree(c.tris);
@@ -281,12 +383,7 @@ void free_scene_buffers(Ctx &c) {
     c.nodes = c.tris = c.shade = c.mats = c.nodes4 = c.nodes4q = c.nodes4h = c.nodes4f = nullptr;
     c.halfVersion = -1;
     c.hybridTop = -1;
-    (void)hipFree(c.runOrder);
-    c.runOrder = nullptr;
-    c.runCount = 0;
-    c.orderKey = Ctx::OrderKey{};
-    c.runCostsValid = false;
-    c.orderFrames = 0;
+    drop_order(c);
     c.sceneVersion = -1;
 }
 
@@ -307,10 +404,14 @@ void destroy_ctx(Ctx &c) {
     (void)hipFree(c.spill);
     c.spill = nullptr;
     c.spillBytes = 0;
+    (void)hipFree(c.exportBuf);
+    c.exportBuf = nullptr;
+    c.exportBytes = 0;
     (void)hipHostFree(c.wfHost);
     for (hipEvent_t e : c.wfPoll)
         if (e) (void)hipEventDestroy(e);
     free_scene_buffers(c);
+    free_retired_tables(c, true);
     for (auto &e : c.pool) {
         (void)hipEventDestroy(e.a);
         (void)hipEventDestroy(e.b);
@@ -414,11 +515,23 @@ unsigned packed_ref_bits(int numNodes, int numPrims) {
     return std::max(bits, 8u);
 }
 
-// The queues' item table of a context's rows (item_order.h): run cost estimates per (scene,
-// camera, image, rows, depth), the table per batch size; rebuilt on the host when one changes.
-bool ensure_order(Ctx &c, const CameraF &cam, int frames, int maxDepth, const char **err) {
+// The queues' item table of a context's rows (item_order.h) for a batch of `frames` frames: run cost
+// estimates per key (scene, camera, image, rows, depth), tables per batch size (kOrderTables of
+// them, so a call's full batches and its remainder batch both stay cached).  With `forced`
+// (HIPPT_OPT_ITEM_ORDER 1) new costs are computed here, on all host threads.  In automatic mode they
+// are computed on a host thread of their own, and the batches queued meanwhile run in image order
+// (*table = nullptr: the same results), so moving the camera never stalls a frame on
+// the estimate (0.34 s single-threaded at 1080p).  A replaced table is freed once the launches
+// that read it are done (an event, not a stream synchronisation).
+constexpr size_t kOrderTables = 4;
+
+int cost_threads() { return int(std::max(1u, std::min(16u, std::thread::hardware_concurrency()))); }
+
+bool ensure_order(Ctx &c, const CameraF &cam, int frames, int maxDepth, bool forced, const unsigned **table,
+                  const char **err) {
     State &s = S();
-    Ctx::OrderKey key;
+    *table = nullptr;
+    OrderKey key;
     key.version = s.scene.version;
     key.width = s.width;
     key.height = s.height;
@@ -427,27 +540,66 @@ bool ensure_order(Ctx &c, const CameraF &cam, int frames, int maxDepth, const ch
     key.stride = c.stride;
     key.maxDepth = maxDepth;
     key.cam = cam;
-    const bool sameCosts = c.runCostsValid && std::memcmp(&key, &c.orderKey, sizeof key) == 0;
-    if (sameCosts && c.runOrder && c.orderFrames == frames) return true;
-    if (!sameCosts) {
-        hippt::run_costs(s.scene.bvh4, reinterpret_cast<const float *>(s.scene.tris.data()), cam, s.width, s.height,
-                         c.y0, c.rows, c.stride, maxDepth, c.runCosts);
+    HIP_TRY(hipSetDevice(c.device));
+    free_retired_tables(c, false);
+    if (!c.runCostsValid || !same_key(key, c.orderKey)) {
+        std::vector<float> cost;
+        if (c.costJob && c.costJob->done.load(std::memory_order_acquire) && same_key(c.costJob->key, key)) {
+            c.costJob->th.join();
+            cost = std::move(c.costJob->cost);
+            c.costJob.reset();
+        } else if (forced) {
+            join_cost_job(c);
+            hippt::run_costs(s.scene.bvh4, reinterpret_cast<const float *>(s.scene.tris.data()), cam, s.width,
+                             s.height, c.y0, c.rows, c.stride, maxDepth, cost, cost_threads());
+        } else {
+            if (c.costJob && c.costJob->done.load(std::memory_order_acquire)) join_cost_job(c);  // a stale key
+            if (!c.costJob) {
+                auto job = std::make_shared<CostJob>();
+                job->key = key;
+                job->bvh = s.scene.bvh4;
+                job->tris = s.scene.tris;
+                CostJob *j = job.get();
+                const int nt = std::max(1, cost_threads() / 2);
+                job->th = std::thread([j, nt] {
+                    hippt::run_costs(j->bvh, reinterpret_cast<const float *>(j->tris.data()), j->key.cam,
+                                     j->key.width, j->key.height, j->key.y0, j->key.rows, j->key.stride,
+                                     j->key.maxDepth, j->cost, nt);
+                    j->done.store(true, std::memory_order_release);
+                });
+                c.costJob = std::move(job);
+            }
+            return true;  // this batch in image order
+        }
+        for (auto &t : c.orderTables) retire_table(c, t.dev);
+        c.orderTables.clear();
+        c.runCosts = std::move(cost);
         c.orderKey = key;
         c.runCostsValid = true;
     }
+    for (size_t k = 0; k < c.orderTables.size(); ++k)
+        if (c.orderTables[k].frames == frames) {
+            std::rotate(c.orderTables.begin(), c.orderTables.begin() + k, c.orderTables.begin() + k + 1);
+            *table = c.orderTables.front().dev;
+            return true;
+        }
     std::vector<uint32_t> order;
     hippt::build_item_table(c.runCosts, unsigned(c.rows) * unsigned(s.width), unsigned(frames), hippt::kMeshQueues,
                             order);
-    HIP_TRY(hipSetDevice(c.device));
-    HIP_TRY(hipStreamSynchronize(c.stream));  // launches in flight read the old table
-    (void)hipFree(c.runOrder);
-    c.runOrder = nullptr;
-    c.runCount = 0;
-    HIP_TRY(hipMalloc(&c.runOrder, std::max<size_t>(1, order.size()) * sizeof(unsigned)));
-    if (!order.empty())
-        HIP_TRY(hipMemcpy(c.runOrder, order.data(), order.size() * sizeof(unsigned), hipMemcpyHostToDevice));
-    c.runCount = unsigned(c.runCosts.size());
-    c.orderFrames = frames;
+    unsigned *dev = nullptr;
+    HIP_TRY(hipMalloc(&dev, std::max<size_t>(1, order.size()) * sizeof(unsigned)));
+    // a fresh buffer: the copy need not wait for the launches queued on the context's stream
+    if (!order.empty() && hipMemcpy(dev, order.data(), order.size() * sizeof(unsigned), hipMemcpyHostToDevice) !=
+                              hipSuccess) {
+        (void)hipFree(dev);
+        return fail(err, "HIP path tracer: item table upload failed");
+    }
+    if (c.orderTables.size() >= kOrderTables) {
+        retire_table(c, c.orderTables.back().dev);
+        c.orderTables.pop_back();
+    }
+    c.orderTables.insert(c.orderTables.begin(), Ctx::OrderTable{frames, dev});
+    *table = dev;
     return true;
 }
 
@@ -585,6 +737,19 @@ bool ensure_spill(Ctx &c, hippt::MeshParams &p, long long blocks, bool spills, i
         c.spillBytes = bytes;
     }
     p.spill = c.spill;
+    return true;
+}
+
+// The drain export's record buffer for `lanes` lanes of a persistent grid (one record each at most).
+bool ensure_export(Ctx &c, size_t lanes, const char **err) {
+    const size_t bytes = lanes * hippt::kExportF4 * sizeof(float4);
+    if (c.exportBytes >= bytes) return true;
+    HIP_TRY(hipStreamSynchronize(c.stream));
+    (void)hipFree(c.exportBuf);
+    c.exportBuf = nullptr;
+    c.exportBytes = 0;
+    HIP_TRY(hipMalloc(&c.exportBuf, bytes));
+    c.exportBytes = bytes;
     return true;
 }
 
@@ -1004,9 +1169,12 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         // (megakernel; item_order.h): Cornell +2.4%, cornell_mixed +3%, blob70k
                         // +0.8% at full size; the slowest 1/8 Cornell share -2% (r5w)
                         if (s.pathMode == 0 && s.itemOrder != 0) {
-                            if (!ensure_order(c, cam, nf, maxDepth, err)) return false;
-                            p.runOrder = c.runOrder;
-                            p.runCount = c.runCount;
+                            const unsigned *table = nullptr;
+                            if (!ensure_order(c, cam, nf, maxDepth, s.itemOrder == 1, &table, err)) return false;
+                            if (table) {
+                                p.runOrder = table;
+                                p.runCount = unsigned(c.runCosts.size());
+                            }
                         }
                         p.poolOffset = unsigned(hippt::mesh_lds_bytes(stackDepth, ldsScene ? numNodes : 0,
                                                                       ldsScene ? numTris : 0, wide, topBytes,
@@ -1025,10 +1193,42 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                                 c.hasDeferred = false;
                             }
                             p.combCtr = c.queue + kCombCtrWord;
+                            // Drain export (not in counting launches: the tail kernels are the timed
+                            // variants)
+                            const int thr = cnt ? 0 : s.drainExport >= 0 ? s.drainExport : kDrainExportAuto;
+                            long long tailBlocks = 0;
+                            if (thr > 0) {
+                                if (!ensure_export(c, size_t(blocks) * hippt::kMeshBlock, err)) return false;
+                                const long long tk = occKey ^ (long long)(spills ? 1 : 0) << 50;
+                                if (c.tailOccKey != tk) {
+                                    const int ln = ldsScene ? numNodes : 0, lt = ldsScene ? numTris : 0,
+                                              lm = ldsScene ? numMats : 0;
+                                    c.tailBlocksPerCu = hippt::mesh_tail_blocks_per_cu(s.scene.full, fmt, stackDepth, ln,
+                                                                                       lt, spills, topBytes, lm);
+                                    c.tailOccKey = tk;
+                                }
+                                const int tbpc = s.tailBlocksPerCu > 0 ? std::min(s.tailBlocksPerCu, c.tailBlocksPerCu)
+                                                                       : std::min(kTailBlocksPerCuAuto, c.tailBlocksPerCu);
+                                tailBlocks = std::min<long long>(blocks, (long long)c.cus * tbpc);
+                                p.exportBuf = c.exportBuf;
+                                p.exportCtr = c.queue + kExportCtrWord;
+                                p.exportClaim = c.queue + kExportClaimWord;
+                                p.exportThr = unsigned(thr);
+                            }
                             EventPair ev;
                             if (!next_events(c, ev, err)) return false;
                             HIP_TRY(hipEventRecord(ev.a, c.stream));
                             HIP_TRY(hippt::launch_mesh(p, int(blocks), cnt, c.stream));
+                            if (thr > 0) {
+                                // the tail launch: the exported paths in full waves
+                                hippt::MeshParams t = p;
+                                t.tailMode = 1;
+                                t.poolWords = 0;
+                                t.poolOffset = 0;
+                                t.comb = hippt::CombineParams{};
+                                t.exportThr = 0;
+                                HIP_TRY(hippt::launch_mesh_tail(t, int(tailBlocks), c.stream));
+                            }
                             HIP_TRY(hipEventRecord(ev.b, c.stream));
                             c.pending.push_back({0, ev});
                         }
@@ -1078,13 +1278,17 @@ bool render_locked(int frameIndex, int count, int maxDepth, const unsigned int *
 }  // namespace
 
 // ---- reference ABI ----------------------------------------------------------------------------
-extern "C" bool cudaPathTracerInit(int width, int height, const char **errorMessage) {
+extern "C" bool cudaPathTracerInit(int width, int height, const char **errorMessage) try {
     std::lock_guard<std::mutex> g(S().mu);
     return init_locked(width, height, errorMessage);
+} catch (const std::exception &e) {
+    return fail_free(errorMessage, e.what());
+} catch (...) {
+    return fail_free(errorMessage, "unknown exception");
 }
 
 extern "C" bool cudaPathTracerRender(int frameIndex, int maxDepth, const unsigned int **hostPixels,
-                                     const char **errorMessage) {
+                                     const char **errorMessage) try {
     std::lock_guard<std::mutex> g(S().mu);
     // the CUDA backend's ABI always hands out its ARGB words (HIPPT_OPT_PIXEL_FORMAT applies to
     // the hippt* render calls)
@@ -1094,32 +1298,48 @@ extern "C" bool cudaPathTracerRender(int frameIndex, int maxDepth, const unsigne
     const bool ok = render_locked(frameIndex, 1, maxDepth, hostPixels, errorMessage);
     s.pixelFormat = format;
     return ok;
+} catch (const std::exception &e) {
+    return fail_free(errorMessage, e.what());
+} catch (...) {
+    return fail_free(errorMessage, "unknown exception");
 }
 
-extern "C" void cudaPathTracerShutdown(void) {
+extern "C" void cudaPathTracerShutdown(void) try {
     std::lock_guard<std::mutex> g(S().mu);
     destroy_all();
+} catch (...) {
+    // an exception must not cross the C ABI (the caller is C or Qt code)
 }
 
-extern "C" bool hipPathTracerInit(int width, int height, const char **errorMessage) {
+extern "C" bool hipPathTracerInit(int width, int height, const char **errorMessage) try {
     return cudaPathTracerInit(width, height, errorMessage);
+} catch (const std::exception &e) {
+    return fail_free(errorMessage, e.what());
+} catch (...) {
+    return fail_free(errorMessage, "unknown exception");
 }
 extern "C" bool hipPathTracerRender(int frameIndex, int maxDepth, const unsigned int **hostPixels,
-                                    const char **errorMessage) {
+                                    const char **errorMessage) try {
     return cudaPathTracerRender(frameIndex, maxDepth, hostPixels, errorMessage);
+} catch (const std::exception &e) {
+    return fail_free(errorMessage, e.what());
+} catch (...) {
+    return fail_free(errorMessage, "unknown exception");
 }
 extern "C" void hipPathTracerShutdown(void) { cudaPathTracerShutdown(); }
 
 // ---- scene --------------------------------------------------------------------------------------
 extern "C" void hipptBuildCamera(const double lookfrom[3], const double lookat[3], const double vup[3],
-                                 double vfovDeg, double aspect, double aperture, double focusDist, hipptCamera *out) {
+                                 double vfovDeg, double aspect, double aperture, double focusDist, hipptCamera *out) try {
     static_assert(sizeof(hipptCamera) == sizeof(CameraF), "camera layout");
     CameraF c;
     build_camera(lookfrom, lookat, vup, vfovDeg, aspect, aperture, focusDist, c);
     std::memcpy(out, &c, sizeof(c));
+} catch (...) {
+    // an exception must not cross the C ABI (the caller is C or Qt code)
 }
 
-extern "C" bool hipptUseBuiltinScene(int sceneId, const char **err) {
+extern "C" bool hipptUseBuiltinScene(int sceneId, const char **err) try {
     std::lock_guard<std::mutex> g(S().mu);
     if (sceneId != HIPPT_SCENE_SPHERE4) return fail(err, "unknown built-in scene id");
     // a pending mesh combine belongs to the image rendered so far: enqueue it before the switch
@@ -1127,13 +1347,17 @@ extern "C" bool hipptUseBuiltinScene(int sceneId, const char **err) {
         if (!flush_deferred(c, err)) return false;
     S().scene.kind = HIPPT_SCENE_SPHERE4;
     return true;
+} catch (const std::exception &e) {
+    return fail_free(err, e.what());
+} catch (...) {
+    return fail_free(err, "unknown exception");
 }
 
 extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int numTris, const float *spheres,
                                  const int *sphereMaterial, int numSpheres, const hipptMaterial *materials,
                                  int numMaterials, const double lookfrom[3], const double lookat[3],
                                  const double vup[3], double vfovDeg, double aperture, double focusDist,
-                                 const char **err) {
+                                 const char **err) try {
     std::lock_guard<std::mutex> g(S().mu);
     State &s = S();
     if (numTris < 0 || numSpheres < 0) return fail(err, "negative primitive count");
@@ -1184,7 +1408,8 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
     hippt::Bvh bvh;
     std::string msg;
     if (!hippt::build_bvh_boxes(boxes.data(), numPrims, extent, bvh, msg, s.bvh)) return fail(err, msg);
-    SceneHost &sc = s.scene;
+    SceneHost sc;  // the new scene, swapped in at the end (a failure keeps the old one)
+    sc.version = s.scene.version;
     sc.nodes.assign(bvh.nodes.size() / 4, float4{});
     std::memcpy(sc.nodes.data(), bvh.nodes.data(), bvh.nodes.size() * sizeof(uint32_t));
     hippt::Bvh4 bvh4;
@@ -1290,13 +1515,18 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
     sc.rawCamera = false;
     sc.kind = HIPPT_SCENE_MESH;
     ++sc.version;
+    s.scene = std::move(sc);
     return true;
+} catch (const std::exception &e) {
+    return fail_free(err, e.what());
+} catch (...) {
+    return fail_free(err, "unknown exception");
 }
 
 extern "C" bool hipptUploadMesh(const float *verts, const int *triMaterial, int numTris, const float *albedo,
                                 int numMaterials, const double lookfrom[3], const double lookat[3],
                                 const double vup[3], double vfovDeg, double aperture, double focusDist,
-                                const char **err) {
+                                const char **err) try {
     if (!albedo) return fail(err, "null scene pointer");
     if (numTris <= 0) return fail(err, "BVH requires at least one triangle");
     std::vector<hipptMaterial> mats(size_t(std::max(0, numMaterials)));
@@ -1305,6 +1535,10 @@ extern "C" bool hipptUploadMesh(const float *verts, const int *triMaterial, int 
                                         1.0f};
     return hipptUploadScene(verts, triMaterial, numTris, nullptr, nullptr, 0, mats.data(), numMaterials, lookfrom,
                             lookat, vup, vfovDeg, aperture, focusDist, err);
+} catch (const std::exception &e) {
+    return fail_free(err, e.what());
+} catch (...) {
+    return fail_free(err, "unknown exception");
 }
 
 namespace {
@@ -1314,13 +1548,12 @@ struct MeshOwner {
 };
 }  // namespace
 
-extern "C" bool hipptReadMesh(const char *path, hipptMesh *out, const char **err) {
+extern "C" bool hipptReadMesh(const char *path, hipptMesh *out, const char **err) try {
     if (!path || !out) return fail(err, "null argument");
     std::memset(out, 0, sizeof(*out));
-    auto *own = new MeshOwner;
+    std::unique_ptr<MeshOwner> own(new MeshOwner);
     std::string msg;
     if (!hippt::read_mesh(path, own->data, msg)) {
-        delete own;
         std::lock_guard<std::mutex> g(S().mu);
         return fail(err, msg);
     }
@@ -1330,32 +1563,46 @@ extern "C" bool hipptReadMesh(const char *path, hipptMesh *out, const char **err
     out->numTris = int(own->data.group.size());
     out->numGroups = int(own->data.groups.size());
     out->groupNames = own->names.data();
-    out->owner_ = own;
+    out->owner_ = own.release();
     return true;
+} catch (const std::exception &e) {
+    return fail_free(err, e.what());
+} catch (...) {
+    return fail_free(err, "unknown exception");
 }
 
-extern "C" void hipptFreeMesh(hipptMesh *mesh) {
+extern "C" void hipptFreeMesh(hipptMesh *mesh) try {
     if (!mesh) return;
     delete static_cast<MeshOwner *>(mesh->owner_);
     std::memset(mesh, 0, sizeof(*mesh));
+} catch (...) {
+    // an exception must not cross the C ABI (the caller is C or Qt code)
 }
 
-extern "C" bool hipptSetCamera(const hipptCamera *camera, const char **err) {
+extern "C" bool hipptSetCamera(const hipptCamera *camera, const char **err) try {
     std::lock_guard<std::mutex> g(S().mu);
     if (!camera) return fail(err, "null camera");
     std::memcpy(&S().scene.cam, camera, sizeof(CameraF));
     S().scene.rawCamera = true;
     return true;
+} catch (const std::exception &e) {
+    return fail_free(err, e.what());
+} catch (...) {
+    return fail_free(err, "unknown exception");
 }
 
 // ---- devices ------------------------------------------------------------------------------------
-extern "C" int hipptDeviceCount(void) {
+extern "C" int hipptDeviceCount(void) try {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;
     return n;
+} catch (const std::exception &e) {
+    return 0;
+} catch (...) {
+    return 0;
 }
 
-extern "C" bool hipptSetDevices(const int *deviceIds, int numDevices, const char **err) {
+extern "C" bool hipptSetDevices(const int *deviceIds, int numDevices, const char **err) try {
     std::lock_guard<std::mutex> g(S().mu);
     State &s = S();
     if (numDevices < 0 || (numDevices > 0 && !deviceIds)) return fail(err, "invalid device list");
@@ -1365,9 +1612,13 @@ extern "C" bool hipptSetDevices(const int *deviceIds, int numDevices, const char
         if (deviceIds[i] < 0 || deviceIds[i] >= avail) return fail(err, "device id out of range");
     s.devices.assign(deviceIds, deviceIds + numDevices);
     return true;
+} catch (const std::exception &e) {
+    return fail_free(err, e.what());
+} catch (...) {
+    return fail_free(err, "unknown exception");
 }
 
-extern "C" bool hipptSetRowRange(int y0, int y1, const char **err) {
+extern "C" bool hipptSetRowRange(int y0, int y1, const char **err) try {
     std::lock_guard<std::mutex> g(S().mu);
     if (y0 < 0 || (y1 > 0 && y1 < y0)) return fail(err, "invalid row range");
     S().rowY0 = y0;
@@ -1375,9 +1626,13 @@ extern "C" bool hipptSetRowRange(int y0, int y1, const char **err) {
     S().rowPhase = 0;
     S().rowStride = 1;
     return true;
+} catch (const std::exception &e) {
+    return fail_free(err, e.what());
+} catch (...) {
+    return fail_free(err, "unknown exception");
 }
 
-extern "C" bool hipptSetRowInterleave(int phase, int stride, const char **err) {
+extern "C" bool hipptSetRowInterleave(int phase, int stride, const char **err) try {
     std::lock_guard<std::mutex> g(S().mu);
     if (stride < 1 || phase < 0 || phase >= stride) return fail(err, "invalid row interleave");
     S().rowPhase = phase;
@@ -1385,26 +1640,42 @@ extern "C" bool hipptSetRowInterleave(int phase, int stride, const char **err) {
     S().rowY0 = 0;
     S().rowY1 = 0;
     return true;
+} catch (const std::exception &e) {
+    return fail_free(err, e.what());
+} catch (...) {
+    return fail_free(err, "unknown exception");
 }
 
 // ---- rendering ----------------------------------------------------------------------------------
 extern "C" bool hipptRenderFrames(int firstFrame, int count, int maxDepth, const unsigned int **hostPixels,
-                                  const char **err) {
+                                  const char **err) try {
     std::lock_guard<std::mutex> g(S().mu);
     return render_locked(firstFrame, count, maxDepth, hostPixels, err);
+} catch (const std::exception &e) {
+    return fail_free(err, e.what());
+} catch (...) {
+    return fail_free(err, "unknown exception");
 }
 
-extern "C" bool hipptRenderFramesAsync(int firstFrame, int count, int maxDepth, const char **err) {
+extern "C" bool hipptRenderFramesAsync(int firstFrame, int count, int maxDepth, const char **err) try {
     std::lock_guard<std::mutex> g(S().mu);
     return enqueue_locked(firstFrame, count, maxDepth, false, err);
+} catch (const std::exception &e) {
+    return fail_free(err, e.what());
+} catch (...) {
+    return fail_free(err, "unknown exception");
 }
 
-extern "C" bool hipptSynchronize(const char **err) {
+extern "C" bool hipptSynchronize(const char **err) try {
     std::lock_guard<std::mutex> g(S().mu);
     return sync_locked(err);
+} catch (const std::exception &e) {
+    return fail_free(err, e.what());
+} catch (...) {
+    return fail_free(err, "unknown exception");
 }
 
-extern "C" bool hipptRenderFramesPresent(int firstFrame, int count, int maxDepth, const char **err) {
+extern "C" bool hipptRenderFramesPresent(int firstFrame, int count, int maxDepth, const char **err) try {
     std::lock_guard<std::mutex> g(S().mu);
     State &s = S();
     if (!s.ready) return fail(err, "HIP path tracer not initialized");
@@ -1426,9 +1697,13 @@ extern "C" bool hipptRenderFramesPresent(int firstFrame, int count, int maxDepth
     s.presentFrames[b] = firstFrame + count;
     s.presentNext = b ^ 1;
     return true;
+} catch (const std::exception &e) {
+    return fail_free(err, e.what());
+} catch (...) {
+    return fail_free(err, "unknown exception");
 }
 
-extern "C" bool hipptLatestFrame(const unsigned int **hostPixels, int *frames, const char **err) {
+extern "C" bool hipptLatestFrame(const unsigned int **hostPixels, int *frames, const char **err) try {
     std::lock_guard<std::mutex> g(S().mu);
     State &s = S();
     if (!s.ready) return fail(err, "HIP path tracer not initialized");
@@ -1452,9 +1727,13 @@ extern "C" bool hipptLatestFrame(const unsigned int **hostPixels, int *frames, c
     if (hostPixels) *hostPixels = s.latest >= 0 ? s.present[s.latest] : nullptr;
     if (frames) *frames = s.latest >= 0 ? s.presentFrames[s.latest] : 0;
     return true;
+} catch (const std::exception &e) {
+    return fail_free(err, e.what());
+} catch (...) {
+    return fail_free(err, "unknown exception");
 }
 
-extern "C" bool hipptReadback(unsigned int *pixels, float *accum, const char **err) {
+extern "C" bool hipptReadback(unsigned int *pixels, float *accum, const char **err) try {
     std::lock_guard<std::mutex> g(S().mu);
     State &s = S();
     if (!s.ready) return fail(err, "HIP path tracer not initialized");
@@ -1466,9 +1745,13 @@ extern "C" bool hipptReadback(unsigned int *pixels, float *accum, const char **e
         HIP_TRY(hipStreamSynchronize(c.stream));
     }
     return true;
+} catch (const std::exception &e) {
+    return fail_free(err, e.what());
+} catch (...) {
+    return fail_free(err, "unknown exception");
 }
 
-extern "C" bool hipptResetAccumulation(const char **err) {
+extern "C" bool hipptResetAccumulation(const char **err) try {
     std::lock_guard<std::mutex> g(S().mu);
     State &s = S();
     if (!s.ready) return fail(err, "HIP path tracer not initialized");
@@ -1480,6 +1763,10 @@ extern "C" bool hipptResetAccumulation(const char **err) {
         HIP_TRY(hipStreamSynchronize(c.stream));
     }
     return true;
+} catch (const std::exception &e) {
+    return fail_free(err, e.what());
+} catch (...) {
+    return fail_free(err, "unknown exception");
 }
 
 // A context's launch counters summed over their kStatSlots copies (hippt_device.h).
@@ -1494,7 +1781,7 @@ bool read_stats(const Ctx &c, unsigned long long (&v)[kStatWords]) {
 }
 
 // ---- counters / options -------------------------------------------------------------------------
-extern "C" bool hipptGetStats(hipptStats *out) {
+extern "C" bool hipptGetStats(hipptStats *out) try {
     std::lock_guard<std::mutex> g(S().mu);
     State &s = S();
     if (!out) return false;
@@ -1518,9 +1805,13 @@ extern "C" bool hipptGetStats(hipptStats *out) {
     out->numTris = s.scene.kind == HIPPT_SCENE_MESH ? s.scene.numTris : 0;
     out->numDevices = int(s.ctxs.size());
     return true;
+} catch (const std::exception &e) {
+    return false;
+} catch (...) {
+    return false;
 }
 
-extern "C" int hipptGetCounters(unsigned long long *out, int n) {
+extern "C" int hipptGetCounters(unsigned long long *out, int n) try {
     std::lock_guard<std::mutex> g(S().mu);
     State &s = S();
     if (!out || n <= 0) return 0;
@@ -1534,9 +1825,13 @@ extern "C" int hipptGetCounters(unsigned long long *out, int n) {
         for (int i = 0; i < n; ++i) out[i] += v[i];
     }
     return n;
+} catch (const std::exception &e) {
+    return 0;
+} catch (...) {
+    return 0;
 }
 
-extern "C" void hipptResetStats(void) {
+extern "C" void hipptResetStats(void) try {
     std::lock_guard<std::mutex> g(S().mu);
     State &s = S();
     const char *err = nullptr;
@@ -1547,9 +1842,11 @@ extern "C" void hipptResetStats(void) {
     }
     s.traceMs = s.combineMs = 0;
     s.traceLaunches = s.combineLaunches = 0;
+} catch (...) {
+    // an exception must not cross the C ABI (the caller is C or Qt code)
 }
 
-extern "C" bool hipptSetOption(int key, long long value) {
+extern "C" bool hipptSetOption(int key, long long value) try {
     std::lock_guard<std::mutex> g(S().mu);
     State &s = S();
     switch (key) {
@@ -1655,16 +1952,32 @@ extern "C" bool hipptSetOption(int key, long long value) {
         if (value < -1 || value > 1) return false;
         s.itemOrder = int(value);
         return true;
+    case HIPPT_OPT_DRAIN_EXPORT:
+        if (value < -1 || value > 64) return false;
+        s.drainExport = int(value);
+        return true;
+    case HIPPT_OPT_TAIL_BLOCKS_PER_CU:
+        if (value < 0 || value > 8) return false;
+        s.tailBlocksPerCu = int(value);
+        return true;
     default: return false;
     }
+} catch (const std::exception &e) {
+    return false;
+} catch (...) {
+    return false;
 }
 
-extern "C" int hipptActiveBvhWidth(void) {
+extern "C" int hipptActiveBvhWidth(void) try {
     std::lock_guard<std::mutex> g(S().mu);
     return S().activeWidth;
+} catch (const std::exception &e) {
+    return 0;
+} catch (...) {
+    return 0;
 }
 
-extern "C" long long hipptGetOption(int key) {
+extern "C" long long hipptGetOption(int key) try {
     std::lock_guard<std::mutex> g(S().mu);
     State &s = S();
     switch (key) {
@@ -1695,17 +2008,23 @@ extern "C" long long hipptGetOption(int key) {
     case HIPPT_OPT_CAMERA_POOL: return s.cameraPool;
     case HIPPT_OPT_FUSE_COMBINE: return s.fuseCombine;
     case HIPPT_OPT_ITEM_ORDER: return s.itemOrder;
+    case HIPPT_OPT_DRAIN_EXPORT: return s.drainExport;
+    case HIPPT_OPT_TAIL_BLOCKS_PER_CU: return s.tailBlocksPerCu;
     case HIPPT_INFO_LDS_TOP_BYTES: return s.activeTopBytes;
     case HIPPT_INFO_BLOCKS_PER_CU: return s.activeBlocksPerCu;
     default: return -1;
     }
+} catch (const std::exception &e) {
+    return -1;
+} catch (...) {
+    return -1;
 }
 
 extern "C" const char *hipptLastError(void) { return S().error; }
 
 // ---- host BVH builder -----------------------------------------------------------------------------
-extern "C" hipptBvh *hipptBvhBuild(const float *verts, int numTris, float extentHint, const char **err) {
-    auto *b = new hipptBvh();
+extern "C" hipptBvh *hipptBvhBuild(const float *verts, int numTris, float extentHint, const char **err) try {
+    std::unique_ptr<hipptBvh> b(new hipptBvh());
     std::string msg;
     hippt::BvhParams params;
     {
@@ -1713,7 +2032,6 @@ extern "C" hipptBvh *hipptBvhBuild(const float *verts, int numTris, float extent
         params = S().bvh;  // the build options an upload would use
     }
     if (!verts || !hippt::build_bvh(verts, numTris, extentHint, b->bvh, msg, params)) {
-        delete b;
         std::lock_guard<std::mutex> g(S().mu);
         fail(err, msg.empty() ? "null vertex pointer" : msg);
         return nullptr;
@@ -1721,28 +2039,46 @@ extern "C" hipptBvh *hipptBvhBuild(const float *verts, int numTris, float extent
     hippt::collapse_bvh4(b->bvh, b->bvh4, params);
     hippt::order_bvh4_top(b->bvh4, kTopOrderNodes);
     (void)hippt::quantize_bvh4(b->bvh4, b->bvh4q);  // empty for boxes near +-FLT_MAX
-    return b;
+    return b.release();
+} catch (const std::exception &e) {
+    return (fail_free(err, e.what()), nullptr);
+} catch (...) {
+    return (fail_free(err, "unknown exception"), nullptr);
 }
 
 extern "C" int hipptBvhNodeCount(const hipptBvh *b) { return b ? int(b->bvh.nodes.size() / hippt::kNodeWords) : 0; }
 extern "C" int hipptBvhDepth(const hipptBvh *b) { return b ? b->bvh.levels : 0; }
-extern "C" void hipptBvhCopy(const hipptBvh *b, uint32_t *nodes, int *triOrder) {
+extern "C" void hipptBvhCopy(const hipptBvh *b, uint32_t *nodes, int *triOrder) try {
     if (!b) return;
     if (nodes) std::memcpy(nodes, b->bvh.nodes.data(), b->bvh.nodes.size() * sizeof(uint32_t));
     if (triOrder) std::memcpy(triOrder, b->bvh.order.data(), b->bvh.order.size() * sizeof(int));
+} catch (...) {
+    // an exception must not cross the C ABI (the caller is C or Qt code)
 }
 extern "C" void hipptBvhFree(hipptBvh *b) { delete b; }
-extern "C" int hipptBvh4NodeCount(const hipptBvh *b) {
+extern "C" int hipptBvh4NodeCount(const hipptBvh *b) try {
     return b ? int(b->bvh4.nodes.size() / hippt::kNode4Words) : 0;
+} catch (const std::exception &e) {
+    return 0;
+} catch (...) {
+    return 0;
 }
 extern "C" int hipptBvh4Depth(const hipptBvh *b) { return b ? b->bvh4.levels : 0; }
 extern "C" int hipptBvh4StackBound(const hipptBvh *b) { return b ? b->bvh4.stackBound : 0; }
-extern "C" void hipptBvh4Copy(const hipptBvh *b, uint32_t *nodes) {
+extern "C" void hipptBvh4Copy(const hipptBvh *b, uint32_t *nodes) try {
     if (b && nodes) std::memcpy(nodes, b->bvh4.nodes.data(), b->bvh4.nodes.size() * sizeof(uint32_t));
+} catch (...) {
+    // an exception must not cross the C ABI (the caller is C or Qt code)
 }
-extern "C" int hipptBvh4QNodeCount(const hipptBvh *b) {
+extern "C" int hipptBvh4QNodeCount(const hipptBvh *b) try {
     return b ? int(b->bvh4q.size() / hippt::kNode4QWords) : 0;
+} catch (const std::exception &e) {
+    return 0;
+} catch (...) {
+    return 0;
 }
-extern "C" void hipptBvh4QCopy(const hipptBvh *b, uint32_t *nodes) {
+extern "C" void hipptBvh4QCopy(const hipptBvh *b, uint32_t *nodes) try {
     if (b && nodes) std::memcpy(nodes, b->bvh4q.data(), b->bvh4q.size() * sizeof(uint32_t));
+} catch (...) {
+    // an exception must not cross the C ABI (the caller is C or Qt code)
 }

@@ -184,6 +184,16 @@ __global__ __launch_bounds__(256) void sphere4_kernel(Sphere4Params P) {
 // [4] HW_ID, [5] XCC_ID
 __device__ unsigned long long g_timeline[65536 * 8];
 #endif
+#ifndef HIPPT_PRIO
+#define HIPPT_PRIO 0
+#endif
+#ifdef HIPPT_DEBUG_RATE
+// per 10 us bucket of a launch (from each wave's own start): [0] samples finished, [1] segments,
+// [2] wave rounds, [3] live-lane rounds (lanes holding a sample), [4] waves running
+// (kRateSlots copies, by wave id, summed on the host: one address per bucket serialised the atomics)
+constexpr int kRateBuckets = 1024, kRateSlots = 256;
+__device__ unsigned long long g_rate[kRateSlots * kRateBuckets * 5];
+#endif
 
 // SGPR budget.  A wave's SGPR allocation (granule 16) plus the 16 the trap handler reserves
 // must fit 7 waves in a SIMD's 800 SGPRs: <= 96.  Unbounded, the compiler used 97-100, the
@@ -279,10 +289,31 @@ __device__ __forceinline__ void pool_take(const MeshParams &P, const float *pool
     }
 }
 
+// A drained wave's live paths into the export buffer (MeshParams::exportBuf), one record per lane
+// holding a sample; a path in mid-traversal restarts its traversal in the tail launch (the closest
+// hit is argmin (t, primitive id): no result bit depends on the traversal's history).
+__device__ __forceinline__ void export_paths(const MeshParams &P, unsigned item, const Ray &r, float tr, float tg,
+                                             float tb, uint32_t rng, int depth) {
+    const bool live = item != kNone;
+    const unsigned long long m = __ballot(live);
+    if (!m) return;
+    const unsigned rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
+    unsigned base = 0;
+    if (__lane_id() == 0) base = atomicAdd(P.exportCtr, unsigned(__popcll(m)));
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (live) {
+        float4 *rec = P.exportBuf + size_t(base + rank) * kExportF4;
+        rec[0] = make_float4(r.ox, r.oy, r.oz, r.dx);
+        rec[1] = make_float4(r.dy, r.dz, tr, tg);
+        rec[2] = make_float4(tb, __uint_as_float(rng), __int_as_float(depth), __uint_as_float(item));
+    }
+}
+
 template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE, bool QUANT, bool SPILL = true, bool POOL = false,
-          bool HYBRID = false, bool HALF = false>
+          bool HYBRID = false, bool HALF = false, bool TAIL = false>
 __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_EU : HIPPT_MESH_WAVES_PER_EU) HIPPT_SGPR_ATTR void mesh_kernel(MeshParams P) {
     static_assert(!QUANT || (WIDE && !LDS_SCENE), "quantized nodes: 4-wide global-memory traversal only");
+    static_assert(!TAIL || !POOL, "the tail launch takes export records, not camera rays");
 #ifdef HIPPT_DEBUG_TIMELINE
     const unsigned tlw = blockIdx.x * 4u + (threadIdx.x >> 6);
     unsigned long long tlDrained = 0, tlItems = 0, tlRounds = 0, tlLate = 0;
@@ -389,7 +420,32 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     // 3.36 -> 3.27 ms, full size unchanged; LDS scenes lose 1% on the share and keep the exit
     // 
     constexpr bool FINISH = POOL && !LDS_SCENE;
+#ifdef HIPPT_DEBUG_RATE
+    const unsigned long long rtStart = __builtin_amdgcn_s_memrealtime();
+    unsigned rtBucket = 0, rtSegs0 = 0, rtSamples0 = 0;
+    unsigned long long rtRounds = 0, rtLive = 0;
+    auto rt_flush = [&](unsigned nb) {
+        const unsigned long long a = wave_sum((unsigned long long)(samples - rtSamples0));
+        const unsigned long long b = wave_sum((unsigned long long)(segs - rtSegs0));
+        rtSamples0 = samples;
+        rtSegs0 = segs;
+        if (__lane_id() == 0) {
+            const unsigned k = ((blockIdx.x * 4u + (threadIdx.x >> 6)) % unsigned(kRateSlots) * unsigned(kRateBuckets) +
+                                min(rtBucket, unsigned(kRateBuckets - 1))) * 5u;
+            atomicAdd(&g_rate[k], a);
+            atomicAdd(&g_rate[k + 1], b);
+            atomicAdd(&g_rate[k + 2], rtRounds);
+            atomicAdd(&g_rate[k + 3], rtLive);
+            atomicAdd(&g_rate[k + 4], 1ull);
+        }
+        rtRounds = rtLive = 0;
+        rtBucket = nb;
+    };
+#endif
     unsigned waveThr = unsigned(P.waveThreshold);
+    // the wave found the queues drained (drain export) / the tail launch's records (TAIL)
+    bool drained = false;
+    const unsigned tailTotal = TAIL ? __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile unsigned *>(P.exportCtr)) : 0u;
     bool combLeft = P.comb.bandPixels != 0;
     if (combLeft && (blockIdx.x & 1u) == 0 && threadIdx.x < 64u)
         while (combLeft) combLeft = combine_chunk(P);
@@ -397,6 +453,14 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         prof<STATS>(pc, 0);
 #ifdef HIPPT_DEBUG_TIMELINE
         if (tlDrained) ++tlRounds;
+#endif
+#ifdef HIPPT_DEBUG_RATE
+        {
+            const unsigned nb = unsigned((__builtin_amdgcn_s_memrealtime() - rtStart) / 1000ull);
+            if (nb != rtBucket) rt_flush(nb);
+            ++rtRounds;
+            rtLive += __popcll(__ballot(item != kNone));
+        }
 #endif
         // ---- refill: every lane whose sample ended takes the next (pixel, frame) -------------
         if (POOL) {
@@ -447,7 +511,44 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                     depth = 0;
                     fresh = true;
                 }
-                if (FINISH && __ballot(took && item == kNone)) waveThr = 0u;
+                if (__ballot(took && item == kNone)) {
+                    drained = true;
+                    if (FINISH) waveThr = 0u;
+                }
+            }
+        } else if (TAIL) {
+            // the tail launch: the next export records for the lanes whose paths ended
+            const unsigned long long m = __ballot(need);
+            if (m) {
+                const unsigned rank =
+                    __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
+                unsigned base = 0;
+                if (__lane_id() == 0) base = atomicAdd(P.exportClaim, unsigned(__popcll(m)));
+                base = __builtin_amdgcn_readfirstlane(base);
+                const unsigned k = base + rank;
+                if (need) {
+                    need = false;
+                    item = kNone;
+                    if (k < tailTotal) {
+                        const float4 *rec = P.exportBuf + size_t(k) * kExportF4;
+                        const float4 a = rec[0], b = rec[1], c = rec[2];
+                        r.ox = a.x;
+                        r.oy = a.y;
+                        r.oz = a.z;
+                        r.dx = a.w;
+                        r.dy = b.x;
+                        r.dz = b.y;
+                        tr = b.z;
+                        tg = b.w;
+                        tb = c.x;
+                        rng = __float_as_uint(c.y);
+                        depth = __float_as_int(c.z);
+                        item = __float_as_uint(c.w);
+                        fresh = true;
+                    }
+                }
+                // records drained: traversals run to the end (no lane can be refilled)
+                if (base + unsigned(__popcll(m)) >= tailTotal) waveThr = 0u;
             }
         } else if (__ballot(need)) {
             const unsigned it = order_item(P, queue_fetch(need, Q, P.queue, P.totalItems, P.chunk));
@@ -455,6 +556,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
             if (!tlDrained && __ballot(need && it == kNone)) tlDrained = __builtin_amdgcn_s_memrealtime();
             tlItems += __popcll(__ballot(it != kNone));
 #endif
+            if (__ballot(need && it == kNone)) drained = true;
             if (need) {
                 need = false;
                 item = it;
@@ -467,6 +569,11 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                 }
             }
         }
+        // drain export: a drained wave with few live paths hands them to the tail launch and leaves
+        if (!TAIL && P.exportThr && drained && unsigned(__popcll(__ballot(item != kNone))) <= P.exportThr) {
+            export_paths(P, item, r, tr, tg, tb, rng, depth);
+            break;
+        }
         // new rays (refilled or scattered): one place, so a pass with lanes of both kinds runs
         // the reciprocals once
         if (fresh) {
@@ -475,6 +582,20 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
             begin(T);
         }
         if (!__any(busy(T) || pend != 0u)) break;
+#if HIPPT_PRIO == 1
+        // issue priority to waves carrying bounced paths over waves of fresh camera rays only
+        if (__ballot(item != kNone && depth > 0)) __builtin_amdgcn_s_setprio(1);
+        else __builtin_amdgcn_s_setprio(0);
+#elif HIPPT_PRIO == 2
+        // by the shallowest bounced path (the most segments possibly left)
+        {
+            const bool b = item != kNone && depth > 0;
+            if (__ballot(b && depth <= 2)) __builtin_amdgcn_s_setprio(3);
+            else if (__ballot(b && depth <= 4)) __builtin_amdgcn_s_setprio(2);
+            else if (__ballot(b)) __builtin_amdgcn_s_setprio(1);
+            else __builtin_amdgcn_s_setprio(0);
+        }
+#endif
 
 
         // ---- traversal: while-while over the BVH; leave once few lanes remain -------------
@@ -485,7 +606,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                     T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit, S, P.topBytes, P.refBits);
             else
                 traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
-        } while (__popcll(__ballot(busy(T))) > (FINISH ? waveThr : unsigned(P.waveThreshold)));
+        } while (__popcll(__ballot(busy(T))) > ((FINISH || TAIL) ? waveThr : unsigned(P.waveThreshold)));
 
         // ---- shading: lanes whose traversal finished (ray_color step, RayTracer.h:579-596) ----
         if (item != kNone && !busy(T)) {
@@ -546,6 +667,9 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     }
 
     while (combLeft) combLeft = combine_chunk(P);
+#ifdef HIPPT_DEBUG_RATE
+    rt_flush(0);
+#endif
 
 #ifdef HIPPT_DEBUG_TIMELINE
     if (__lane_id() == 0 && tlw < 65536) {
@@ -619,6 +743,25 @@ extern "C" int hipptDebugTimeline(unsigned long long *out, int maxWaves) {
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_timeline), size_t(n) * 8 * sizeof(unsigned long long)) == hipSuccess
                ? n
                : -1;
+}
+#endif
+
+#ifdef HIPPT_DEBUG_RATE
+extern "C" int hipptDebugRate(unsigned long long *out, int reset) {
+    static unsigned long long buf[kRateSlots * kRateBuckets * 5];
+    if (out) {
+        if (hipMemcpyFromSymbol(buf, HIP_SYMBOL(g_rate), sizeof(buf)) != hipSuccess) return -1;
+        for (int i = 0; i < kRateBuckets * 5; ++i) {
+            unsigned long long v = 0;
+            for (int k = 0; k < kRateSlots; ++k) v += buf[size_t(k) * kRateBuckets * 5 + i];
+            out[i] = v;
+        }
+    }
+    if (reset) {
+        std::fill(buf, buf + kRateSlots * kRateBuckets * 5, 0ull);
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_rate), buf, sizeof(buf)) != hipSuccess) return -1;
+    }
+    return kRateBuckets;
 }
 #endif
 
@@ -699,6 +842,51 @@ hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hip
     }
     hipLaunchKernelGGL(fn, dim3(blocks), dim3(kMeshBlock), bytes, s, p);
     return hipGetLastError();
+}
+
+// The tail launch's kernels: the timed (non-counting) variants without the camera-ray pool.
+static MeshFn mesh_fn_tail(bool lds, bool full, int fmt, bool spill) {
+#define HIPPT_TAIL_FN(FULL_, SPILL_)                                                                              \
+    (lds ? (fmt == kWide2 ? mesh_kernel<false, true, FULL_, false, false, SPILL_, false, false, false, true>        \
+                          : mesh_kernel<false, true, FULL_, true, false, SPILL_, false, false, false, true>)       \
+     : fmt == kWide2       ? mesh_kernel<false, false, FULL_, false, false, SPILL_, false, false, false, true>      \
+     : fmt == kWideQuant   ? mesh_kernel<false, false, FULL_, true, true, SPILL_, false, false, false, true>       \
+     : fmt == kWideHybrid  ? mesh_kernel<false, false, FULL_, true, true, SPILL_, false, true, false, true>        \
+     : fmt == kWideHalf    ? mesh_kernel<false, false, FULL_, true, false, SPILL_, false, false, true, true>       \
+                           : mesh_kernel<false, false, FULL_, true, false, SPILL_, false, false, false, true>)
+    // 2-wide trees have no stack cap: their kernels keep the spill code path (SPILL = true)
+    if (full) return spill || fmt == kWide2 ? HIPPT_TAIL_FN(true, true) : HIPPT_TAIL_FN(true, false);
+    return spill || fmt == kWide2 ? HIPPT_TAIL_FN(false, true) : HIPPT_TAIL_FN(false, false);
+#undef HIPPT_TAIL_FN
+}
+
+hipError_t launch_mesh_tail(const MeshParams &p, int blocks, hipStream_t s) {
+    if (!p.tailMode || !p.exportBuf || !p.exportCtr || !p.exportClaim || p.poolWords || p.comb.bandPixels)
+        return hipErrorInvalidValue;
+    if (p.stackDepth < 1 || p.stackDepth > kStackDepth) return hipErrorInvalidValue;
+    if (p.wide && (p.stackCap < 1 || p.stackCap + 2 > p.stackDepth)) return hipErrorInvalidValue;
+    const bool lds = p.ldsScene != 0;
+    if (p.wide < kWide2 || p.wide > kWideHalf || (lds && p.wide >= kWideQuant)) return hipErrorInvalidValue;
+    const size_t bytes = mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0, p.wide != 0, p.topBytes,
+                                        lds ? p.numMats : 0, 0);
+    const MeshFn fn = mesh_fn_tail(lds, p.full != 0, p.wide, p.spill != nullptr);
+    if (p.wide && (lds || p.topBytes)) {
+        const hipError_t e = check_lds_at_zero(reinterpret_cast<const void *>(fn));
+        if (e != hipSuccess) return e;
+    }
+    hipLaunchKernelGGL(fn, dim3(blocks), dim3(kMeshBlock), bytes, s, p);
+    return hipGetLastError();
+}
+
+int mesh_tail_blocks_per_cu(bool full, int fmt, int stackDepth, int ldsNodes, int ldsTris, bool spill, unsigned topBytes,
+                            int ldsMats) {
+    int n = 0;
+    const bool lds = ldsNodes > 0;
+    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, fmt != kWide2, topBytes, ldsMats, 0);
+    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
+        &n, mesh_fn_tail(lds, full, lds && fmt >= kWideQuant ? kWideFloat : fmt, spill), kMeshBlock, bytes);
+    if (e != hipSuccess || n <= 0) n = 1;
+    return std::min(n, kMaxResidentBlocks);
 }
 
 hipError_t launch_combine(const CombineParams &p, hipStream_t s, const HostFrame &h) {

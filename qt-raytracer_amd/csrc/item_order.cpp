@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <thread>
 #include <utility>
 
 namespace hippt {
@@ -134,27 +135,41 @@ double sample_cost(const Bvh4 &b, const float *tris, D3 o, D3 d, int maxDepth) {
 }  // namespace
 
 void run_costs(const Bvh4 &bvh, const float *tris, const CameraF &cam, int width, int height, int y0, int rows,
-               int stride, int maxDepth, std::vector<float> &cost) {
+               int stride, int maxDepth, std::vector<float> &cost, int threads) {
     cost.clear();
     if (width <= 0 || rows <= 0) return;
     const size_t runs = size_t(rows) * size_t(width) / 64;
     const double sw = double(std::max(1, width - 1)), sh = double(std::max(1, height - 1));
     const D3 O{cam.origin[0], cam.origin[1], cam.origin[2]};
     cost.assign(runs, 0.0f);
-    for (size_t r = 0; r < runs; ++r) {
-        double c = 0.0;
-        for (int j = 0; j < 4; ++j) {
-            const size_t p = 64 * r + size_t(21 * j);  // band pixels 0, 21, 42, 63 of the run
-            const double x = double(p % size_t(width)) + 0.5;
-            const double y = double(y0 + int(p / size_t(width)) * stride) + 0.5;
-            const double s = x / sw, t = y / sh;
-            const D3 d{cam.llc[0] + s * cam.horizontal[0] + t * cam.vertical[0] - O.x,
-                       cam.llc[1] + s * cam.horizontal[1] + t * cam.vertical[1] - O.y,
-                       cam.llc[2] + s * cam.horizontal[2] + t * cam.vertical[2] - O.z};
-            c += sample_cost(bvh, tris, O, d, std::max(1, maxDepth));
+    auto span = [&](size_t r0, size_t r1) {
+        for (size_t r = r0; r < r1; ++r) {
+            double c = 0.0;
+            for (int j = 0; j < 4; ++j) {
+                const size_t p = 64 * r + size_t(21 * j);  // band pixels 0, 21, 42, 63 of the run
+                const double x = double(p % size_t(width)) + 0.5;
+                const double y = double(y0 + int(p / size_t(width)) * stride) + 0.5;
+                const double s = x / sw, t = y / sh;
+                const D3 d{cam.llc[0] + s * cam.horizontal[0] + t * cam.vertical[0] - O.x,
+                           cam.llc[1] + s * cam.horizontal[1] + t * cam.vertical[1] - O.y,
+                           cam.llc[2] + s * cam.horizontal[2] + t * cam.vertical[2] - O.z};
+                c += sample_cost(bvh, tris, O, d, std::max(1, maxDepth));
+            }
+            cost[r] = float(c / 4.0);
         }
-        cost[r] = float(c / 4.0);
+    };
+    // each run's estimate is independent of the others: contiguous spans per thread (same values
+    // for any thread count)
+    const size_t nt = std::min<size_t>(size_t(std::max(1, threads)), std::max<size_t>(1, runs / 256));
+    if (nt <= 1) {
+        span(0, runs);
+        return;
     }
+    std::vector<std::thread> pool;
+    pool.reserve(nt - 1);
+    for (size_t k = 1; k < nt; ++k) pool.emplace_back(span, runs * k / nt, runs * (k + 1) / nt);
+    span(0, runs / nt);
+    for (auto &t : pool) t.join();
 }
 
 void build_item_table(const std::vector<float> &cost, unsigned bandPixels, unsigned frames, unsigned queues,

@@ -22,6 +22,11 @@ them changes the bytes but not the statistics the tests check):
                 (running-average recurrence of CudaPathTracerKernel.cu:157-178 over frames 0..63).
                 Not the reference binary (CUDA is unbuildable here): the oracle pinned by the
                 other targets.  Minutes of CPU (all cores); not part of the default targets.
+  headline4k    oracle_headline4k_blob70k_3840x2160_256.json: BASELINE configs[3]'s image (blob70k,
+                3840x2160, 256 spp, 8 bounces) on HEADLINE4K_ROWS, 16 rows through the top, the
+                mesh, the bottom and row 1610 (pixel (1750, 1610) starts a short RNG cycle in
+                frame 17): per row the ARGB CRC32, the SHA-256 of its accumulation floats after
+                all 256 frames, segments and pixel samples.  ~4 minutes of CPU (8 cores).
 Fixtures are data only: inputs and the reference's outputs.
 """
 from __future__ import annotations
@@ -112,6 +117,37 @@ def make_headline(only=None) -> None:
         print(name, "crc32", d["image_crc32"], "segments", segs, f"{time.time() - t0:.0f} s")
 
 
+# BASELINE configs[3]: rows of the 4K / 256 spp image pinned by the headline4k target
+HEADLINE4K = ("blob70k", 3840, 2160, 256, 8)
+HEADLINE4K_ROWS = [0, 1, 270, 540, 700, 810, 900, 1000, 1080, 1200, 1350, 1500, 1610, 1800, 2000, 2159]
+
+
+def headline4k_path():
+    name, w, h, spp, _ = HEADLINE4K
+    return os.path.join(HERE, f"oracle_headline4k_{name}_{w}x{h}_{spp}.json")
+
+
+def make_headline4k() -> None:
+    import hashlib
+    import time
+    import zlib
+    name, w, h, spp, depth = HEADLINE4K
+    t0 = time.time()
+    ms = pyoracle.MeshScene(scenes.get_scene(name), w, h, accel=1)
+    rows = []
+    for y in HEADLINE4K_ROWS:
+        px, acc, segs, samples = ms.frames(0, spp, depth, y0=y, y1=y + 1, nthreads=os.cpu_count() or 1)
+        rows.append({"y": y, "crc32": zlib.crc32(px.tobytes()) & 0xFFFFFFFF,
+                     "accum_sha256": hashlib.sha256(acc.tobytes()).hexdigest(), "segments": segs,
+                     "pixel_samples": samples})
+        print(name, "row", y, rows[-1]["crc32"], segs, f"{time.time() - t0:.0f} s", flush=True)
+    d = {"scene": name, "width": w, "height": h, "spp": spp, "max_depth": depth,
+         "generator": "oracle/pt_oracle.c po_mesh_frames (FP32 restatement), tests/golden/make_golden.py headline4k",
+         "rows": rows}
+    with open(headline4k_path(), "w") as f:
+        json.dump(d, f, indent=0)
+
+
 def main() -> None:
     ap = argparse.ArgumentParser()
     ap.add_argument("targets", nargs="*", default=["functions", "random_scene", "converge"])
@@ -120,7 +156,9 @@ def main() -> None:
     a = ap.parse_args()
     if "headline" in a.targets:
         make_headline(a.scenes)
-    if set(a.targets) - {"headline"} and not os.path.exists(pyoracle.REF_HARNESS_STRICT):
+    if "headline4k" in a.targets:
+        make_headline4k()
+    if set(a.targets) - {"headline", "headline4k"} and not os.path.exists(pyoracle.REF_HARNESS_STRICT):
         raise SystemExit("oracle/_ref not built: make -C oracle ref (needs /root/reference)")
     tmp = tempfile.mkdtemp()
     if "functions" in a.targets:

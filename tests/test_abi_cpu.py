@@ -3,6 +3,7 @@ import ctypes
 import os
 import re
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -91,6 +92,8 @@ def test_options_validate():
     (hippt.OPT_ITEM_ORDER, (-1, 0, 1), (-2, 2), -1),
     (hippt.OPT_STACK_CAP, (0, 4, 30), (3, 31), 0),
     (hippt.OPT_BVH_QUANT, (-1, 0, 1, 2, 3), (-2, 4), -1),
+    (hippt.OPT_DRAIN_EXPORT, (-1, 0, 16, 64), (-2, 65), -1),
+    (hippt.OPT_TAIL_BLOCKS_PER_CU, (0, 1, 8), (-1, 9), 0),
 ])
 def test_round2_options_round_trip(key, good, bad, default):
     """Each option accepts its documented range (include/hippt.h), reads back what was set,
@@ -130,3 +133,45 @@ def test_mesh_upload_validates_inputs():
 
 def test_device_count_without_gpu_is_safe():
     assert hippt.device_count() >= 0
+
+
+_OOM_CHILD = r"""
+import ctypes, resource, sys
+sys.path.insert(0, sys.argv[1])
+import numpy as np
+import hippt
+from hippt import scenes
+lib = hippt.load_library()
+sc = scenes.blob70k()
+v = np.ascontiguousarray(sc.verts, np.float32).reshape(-1, 9)
+m = np.ascontiguousarray(sc.tri_mat, np.int32)
+a = np.ascontiguousarray(sc.albedo, np.float32).reshape(-1, 3)
+d3 = lambda t: (ctypes.c_double * 3)(*t)
+def upload():
+    e = ctypes.c_char_p()
+    ok = lib.hipptUploadMesh(v.ctypes.data_as(ctypes.POINTER(ctypes.c_float)),
+                             m.ctypes.data_as(ctypes.POINTER(ctypes.c_int)), v.shape[0],
+                             a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)), a.shape[0], d3(sc.lookfrom),
+                             d3(sc.lookat), d3(sc.vup), float(sc.vfov), float(sc.aperture), float(sc.focus),
+                             ctypes.byref(e))
+    return ok, e.value
+assert upload()[0]  # the same upload succeeds without the limit
+vm = int(open("/proc/self/status").read().split("VmSize:")[1].split()[0]) * 1024
+resource.setrlimit(resource.RLIMIT_AS, (vm + (4 << 20), resource.RLIM_INFINITY))
+ok, msg = upload()
+resource.setrlimit(resource.RLIMIT_AS, (resource.RLIM_INFINITY, resource.RLIM_INFINITY))
+print("RESULT", ok, msg)
+assert not ok and msg and msg.startswith(b"HIP path tracer:"), (ok, msg)
+"""
+
+
+def test_allocation_failure_returns_false_not_terminate(tmp_path):
+    """an exception inside an extern "C" entry point (here std::bad_alloc from the host
+    BVH build of a valid blob70k upload under a lowered RLIMIT_AS) must come back as the reference's
+    false + message convention (CudaPathTracerKernel.cu:181-184), not std::terminate the caller."""
+    script = tmp_path / "oom_child.py"
+    script.write_text(_OOM_CHILD)
+    r = subprocess.run([sys.executable, str(script), os.path.join(REPO, "qt-raytracer_amd")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    assert "RESULT False" in r.stdout

@@ -8,6 +8,10 @@
   (hipptSetDevices([0]*8), interleaved rows) and 8 one-process-per-GPU shares
   (hipptSetRowInterleave(r, 8), gathered on the host) each give the one-context image bit for bit,
   and sampled rows equal the oracle.  2 spp keeps the oracle's rows to seconds.
+* configs[3] at its real sample count (3840x2160, 256 spp, 8 bounces): 16 rows of the image (top,
+  through the mesh, bottom, and row 1610, whose pixel (1750, 1610) starts a short RNG cycle in
+  frame 17) equal the oracle's rows after all 256 frames (tests/golden/make_golden.py headline4k),
+  rendered as one context and as 8 hipptSetRowInterleave(r, 8) shares.
 """
 import json
 import os
@@ -97,3 +101,36 @@ def test_config4_row_split_on_one_gpu(pt):
         ora = ms.frames(0, spp, depth, y0=y0, y1=y0 + 2)
         assert np.array_equal(one[0][y0:y0 + 2], ora[0])
         assert one[1][y0:y0 + 2].tobytes() == ora[1].tobytes()
+
+
+def test_config4_full_spp_rows_equal_oracle_golden(pt):
+    """configs[3]'s job at 256 spp: the frames 2..255 that the 2-spp split test above leaves out,
+    including the short-cycle escape pixel, against the oracle's running average
+    (CudaPathTracerKernel.cu:157-178) of all 256 frames, as one image and as the 8-way row split."""
+    import hashlib
+    with open(os.path.join(GOLDEN, "oracle_headline4k_blob70k_3840x2160_256.json")) as f:
+        g = json.load(f)
+    w, h, spp, depth = g["width"], g["height"], g["spp"], g["max_depth"]
+    pt.uploadMesh(scenes.get_scene(g["scene"]))
+
+    def check(px, acc, rows, what):
+        for r in rows:
+            y = r["y"]
+            assert zlib.crc32(px[y].tobytes()) & 0xFFFFFFFF == r["crc32"], f"{what}: row {y} differs"
+            assert hashlib.sha256(acc[y].tobytes()).hexdigest() == r["accum_sha256"], f"{what}: row {y}"
+
+    assert pt.initialize(w, h), pt.lastError()
+    assert pt.renderFramesAsync(spp, depth), pt.lastError()
+    px, acc = pt.readback()
+    check(px, acc, g["rows"], "one context")
+    n = 8
+    for k in range(n):
+        rows = [r for r in g["rows"] if r["y"] % n == k]
+        if not rows:
+            continue
+        pt.setRowInterleave(k, n)
+        assert pt.initialize(w, h), pt.lastError()
+        pt.resetStats()
+        assert pt.renderFramesAsync(spp, depth), pt.lastError()
+        px, acc = pt.readback()
+        check(px, acc, rows, f"share {k}/{n}")

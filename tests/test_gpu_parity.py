@@ -30,7 +30,8 @@ def pt():
                  (hippt.OPT_STACK_CAP, 0), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_LDS_TOP_NODES, -1),
                  (hippt.OPT_RNG_TABLE, 0), (hippt.OPT_BVH_COLLAPSE, -1), (hippt.OPT_BVH_NODE_COST, 200),
                  (hippt.OPT_BVH_LEAF4, 4), (hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_ARGB),
-                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1), (hippt.OPT_ITEM_ORDER, -1)):
+                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1), (hippt.OPT_ITEM_ORDER, -1),
+                 (hippt.OPT_DRAIN_EXPORT, -1), (hippt.OPT_TAIL_BLOCKS_PER_CU, 0)):
         t.setOption(k, v)
     t.resetStats()
     yield t
@@ -213,6 +214,18 @@ def test_wavefront_large_pools_equal_megakernel(pt, slots, w, h, spp):
     (a, sa), (b, sb) = got
     assert sa == sb
     _assert_same(a[0], a[1], b[0], b[1])
+    if (w, h, spp) == (1920, 1080, 64):
+        # configs[4]'s wavefront image against configs[2]'s oracle golden directly, not only
+        # through the megakernel
+        import hashlib
+        import json
+        import zlib
+        with open(os.path.join(os.path.dirname(__file__), "golden",
+                               "oracle_headline_blob70k_1920x1080_64.json")) as f:
+            g = json.load(f)
+        assert zlib.crc32(b[0].tobytes()) & 0xFFFFFFFF == g["image_crc32"]
+        assert hashlib.sha256(b[1].tobytes()).hexdigest() == g["accum_sha256"]
+        assert sb == g["segments"]
 
 
 def test_wavefront_pools_on_a_shared_device(pt):
@@ -482,6 +495,68 @@ def test_item_order_does_not_change_results(pt, name, w, h, frames):
     rows = np.arange(1, h, 3)
     _assert_same(got[0][rows], got[1][rows], ora[0][rows], ora[1][rows])
     pt.setRowRange(0, 0)
+
+
+def test_item_order_camera_change_does_not_stall(pt):
+    """in automatic mode (HIPPT_OPT_ITEM_ORDER -1) a camera change does not stall the next
+    call on the host's run-cost estimate (0.34 s single-threaded at 1080p): the estimate runs on a
+    host thread of its own and the batches queued meanwhile run in image order.  Every call's image
+    is the oracle's, before, during and after the switch to the new order; calls with batches of
+    different sizes reuse their tables."""
+    import ctypes
+    import time
+    sc = scenes.cornell34()
+    w, h = 1920, 1080
+    pt.uploadMesh(sc)
+    assert pt.initialize(w, h), pt.lastError()
+    assert pt.renderFrames(1, 8, copy=False), pt.lastError()
+    moved = dict(lookfrom=(sc.lookfrom[0] + 40.0, sc.lookfrom[1] + 25.0, sc.lookfrom[2]), lookat=sc.lookat,
+                 vup=sc.vup, vfov=sc.vfov, aspect=w / h, aperture=sc.aperture, focus=sc.focus)
+    cam = hippt.build_camera(**moved)
+    lib = hippt.load_library()
+    err = ctypes.c_char_p()
+    assert lib.hipptSetCamera(ctypes.byref(cam), ctypes.byref(err)), err.value
+    t0 = time.perf_counter()
+    assert pt.renderFramesAsync(1, 8), pt.lastError()
+    assert pt.synchronize()
+    first = time.perf_counter() - t0
+    assert first < 0.15, f"first call after the camera change took {first:.3f} s"
+    # small image: the oracle's frames for the moved camera, through the switch to the new order
+    pt.resetAccumulation()
+    ws, hs = 160, 90
+    sc2 = scenes.cornell34()
+    sc2.lookfrom = moved["lookfrom"]
+    ora = po.MeshScene(sc2, ws, hs).frames(0, 3, 8)
+    pt.uploadMesh(sc2)
+    assert pt.initialize(ws, hs), pt.lastError()
+    for _ in range(20):  # the first calls in image order, later ones (the estimate done) in cost order
+        assert pt.renderFrames(3, 8), pt.lastError()
+        got = pt.readback()
+        _assert_same(got[0], got[1], ora[0], ora[1])
+        time.sleep(0.005)
+
+
+@pytest.mark.parametrize("name,w,h,frames", [("cornell34", 200, 77, 3), ("blob70k", 131, 64, 2),
+                                               ("cornell_mixed", 96, 53, 2), ("random_scene", 77, 41, 2)])
+def test_drain_export_does_not_change_results(pt, name, w, h, frames):
+    """HIPPT_OPT_DRAIN_EXPORT: drained waves with at most N live paths hand them (ray, throughput, RNG
+    state, depth, item) to a second, small launch of the same batch, which finishes them with full
+    lanes; the image and the counts are the oracle's for every threshold (64: every drained wave
+    exports) and tail-launch size, with the camera pool on and off."""
+    sc = scenes.get_scene(name)
+    ora = po.MeshScene(sc, w, h).frames(0, frames, 8)
+    pt.uploadMesh(sc)
+    for thr, bpc, pool in ((64, 1, -1), (16, 0, -1), (32, 8, 0), (64, 2, 0)):
+        pt.setOption(hippt.OPT_DRAIN_EXPORT, thr)
+        pt.setOption(hippt.OPT_TAIL_BLOCKS_PER_CU, bpc)
+        pt.setOption(hippt.OPT_CAMERA_POOL, pool)
+        assert pt.initialize(w, h), pt.lastError()
+        assert pt.renderFrames(frames, 8), pt.lastError()
+        got = pt.readback()
+        _assert_same(got[0], got[1], ora[0], ora[1])
+        st = pt.stats()
+        assert st["segments"] == ora[2] and st["pixelSamples"] == ora[3]
+        pt.resetStats()
 
 
 @pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene"])
