@@ -763,7 +763,7 @@ uint16_t half_round_down(float x) {
 
 uint16_t half_round_up(float x) { return uint16_t(half_round_down(-x) ^ 0x8000u); }
 
-void half_bvh4(const uint32_t *in, size_t numNodes, std::vector<uint32_t> &out) {
+bool half_bvh4(const uint32_t *in, size_t numNodes, std::vector<uint32_t> &out) {
     out.assign(numNodes * kNode4Words, 0u);
     for (size_t k = 0; k < numNodes; ++k) {
         const uint32_t *w = in + k * kNode4Words;
@@ -773,6 +773,13 @@ void half_bvh4(const uint32_t *in, size_t numNodes, std::vector<uint32_t> &out) 
                 float lo, hi;
                 std::memcpy(&lo, w + 8 * a + i, 4);
                 std::memcpy(&hi, w + 8 * a + 4 + i, 4);
+                // a finite plane beyond the half range would round to an infinite one: a box every
+                // ray enters.  No half tree then (the caller keeps float nodes), like quantize_bvh4
+                // for boxes no 8-bit grid covers.
+                if ((std::isfinite(lo) && lo < -65504.0f) || (std::isfinite(hi) && hi > 65504.0f)) {
+                    out.clear();
+                    return false;
+                }
                 const uint16_t l = half_round_down(lo), u = half_round_up(hi);
                 h[16 * a + i] = l;  // [lo hi]: positive direction
                 h[16 * a + 4 + i] = u;
@@ -781,6 +788,7 @@ void half_bvh4(const uint32_t *in, size_t numNodes, std::vector<uint32_t> &out) 
             }
         std::memcpy(out.data() + k * kNode4Words + 24, w + 24, 16);  // codes at byte 96
     }
+    return true;
 }
 
 }  // namespace hippt

@@ -108,11 +108,13 @@ bool hybrid_bvh4(const Bvh4 &b, const std::vector<uint32_t> &q, int topNodes, st
 // with a positive direction on a, then [hi[4] lo[4]] for negative ones, so the octant's near and
 // far planes are ONE aligned 16-byte read at the float node's near-row address (near planes in its
 // words 0-1, far planes in words 2-3).  Bytes 96-111 the child codes (Bvh4 words 24-27), 112-127
-// zero.  Planes are rounded outward (lo down, hi up; beyond the half range to -inf / +inf), so
+// zero.  Planes are rounded outward (lo down, hi up; only the empty slots' infinite planes stay infinite), so
 // every box contains the Bvh4 box and a kernel's slab test of it (v_fma_mix_f32: the half enters
 // the FMA exactly) is the float node's test of a larger box.
-// `in` is kNode4Words per node, in any code convention (the code words are copied).
-void half_bvh4(const uint32_t *in, size_t numNodes, std::vector<uint32_t> &out);
+// `in` is kNode4Words per node, in any code convention (the code words are copied).  Returns false
+// (and leaves `out` empty) when a finite lo plane lies below -65504 or a finite hi plane above
+// 65504: its half would be infinite, a box every ray enters; such scenes keep float nodes.
+bool half_bvh4(const uint32_t *in, size_t numNodes, std::vector<uint32_t> &out);
 uint16_t half_round_down(float x);  // the largest half <= x (x not NaN)
 uint16_t half_round_up(float x);    // the smallest half >= x
 float half_value(uint16_t h);

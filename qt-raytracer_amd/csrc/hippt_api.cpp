@@ -180,6 +180,7 @@ struct SceneHost {
     std::vector<float4> nodes4;                 // 4-wide BVH (bvh_builder.h Bvh4)
     std::vector<float4> nodes4q;                // quantize_bvh4 of it
     std::vector<float4> nodes4f;                // half_bvh4 of it (device codes; built on use)
+    int halfState = 0;                          // nodes4f: 0 not built, 1 built, -1 out of half range
     hippt::Bvh4 bvh4;                           // the 4-wide tree with node-index codes ...
     std::vector<uint32_t> q4;                   // ... and its 8-bit nodes (hybrid_bvh4 inputs)
     std::vector<float4> hybrid;                 // hybrid_bvh4 for hybridTop top nodes (built on use)
@@ -604,15 +605,25 @@ bool ensure_order(Ctx &c, const CameraF &cam, int frames, int maxDepth, bool for
 }
 
 // The half-precision node layout (bvh_builder.h half_bvh4, HIPPT_OPT_BVH_QUANT 3): built on the host
-// once per scene and uploaded to a context's device the first time a render there uses it.
+// once per scene (half_tree_ok) and uploaded to a context's device the first time a render there
+// uses it.
+bool half_tree_ok(SceneHost &sc) {
+    if (sc.halfState == 0) {
+        std::vector<uint32_t> h;
+        if (hippt::half_bvh4(reinterpret_cast<const uint32_t *>(sc.nodes4.data()), size_t(sc.numNodes4), h)) {
+            sc.nodes4f.assign(h.size() / 4, float4{});
+            std::memcpy(sc.nodes4f.data(), h.data(), h.size() * sizeof(uint32_t));
+            sc.halfState = 1;
+        } else {
+            sc.halfState = -1;  // planes beyond the half range: float nodes
+        }
+    }
+    return sc.halfState > 0;
+}
+
 bool ensure_half(Ctx &c, const char **err) {
     SceneHost &sc = S().scene;
-    if (sc.nodes4f.empty()) {
-        std::vector<uint32_t> h;
-        hippt::half_bvh4(reinterpret_cast<const uint32_t *>(sc.nodes4.data()), size_t(sc.numNodes4), h);
-        sc.nodes4f.assign(h.size() / 4, float4{});
-        std::memcpy(sc.nodes4f.data(), h.data(), h.size() * sizeof(uint32_t));
-    }
+    if (!half_tree_ok(sc)) return fail(err, "HIP path tracer: no half-precision tree for this scene");
     if (c.halfVersion == sc.version && c.nodes4f) return true;
     HIP_TRY(hipSetDevice(c.device));
     HIP_TRY(hipStreamSynchronize(c.stream));
@@ -1034,7 +1045,8 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                               (s.bvhQuant == -1 && !s.scene.full && s.pathMode == 1));
                 // Half-precision planes (HIPPT_OPT_BVH_QUANT 3, megakernel and wavefront extend): the
                 // float nodes' size and codes, 4 reads per visit instead of 7
-                const bool half = wide && !ldsScene && s.bvhQuant == 3;
+                // half planes unless the scene's planes leave the half range (then float nodes)
+                const bool half = wide && !ldsScene && s.bvhQuant == 3 && half_tree_ok(s.scene);
                 // The top of a global-memory tree in LDS (megakernel and wavefront extend): the
                 // breadth-first prefix of the node array that the LDS budget of the resident blocks
                 // leaves beside the stack (automatic), or HIPPT_OPT_LDS_TOP_NODES nodes.  The
@@ -1457,6 +1469,7 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
     byte_codes(sc.nodes4, hippt::kNode4Words, 24, hippt::kNode4Words * 4);
     byte_codes(sc.nodes4q, hippt::kNode4QWords, 12, hippt::kNode4QWords * 4);
     sc.nodes4f.clear();
+    sc.halfState = 0;
     sc.levels4 = bvh4.levels;
     sc.stackBound4 = bvh4.stackBound;
     sc.tris.assign(size_t(numPrims) * 3, float4{});

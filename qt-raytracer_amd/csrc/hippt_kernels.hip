@@ -184,9 +184,6 @@ __global__ __launch_bounds__(256) void sphere4_kernel(Sphere4Params P) {
 // [4] HW_ID, [5] XCC_ID
 __device__ unsigned long long g_timeline[65536 * 8];
 #endif
-#ifndef HIPPT_PRIO
-#define HIPPT_PRIO 0
-#endif
 #ifdef HIPPT_DEBUG_RATE
 // per 10 us bucket of a launch (from each wave's own start): [0] samples finished, [1] segments,
 // [2] wave rounds, [3] live-lane rounds (lanes holding a sample), [4] waves running
@@ -418,7 +415,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     // the queues drained, its traversal rounds run until no lane traverses (no wave-threshold
     // exit), so its last iterations are not one node visit each: the slowest 1/8 blob70k share
     // 3.36 -> 3.27 ms, full size unchanged; LDS scenes lose 1% on the share and keep the exit
-    // 
+    // (DESIGN_LOG.md §A.1)
     constexpr bool FINISH = POOL && !LDS_SCENE;
 #ifdef HIPPT_DEBUG_RATE
     const unsigned long long rtStart = __builtin_amdgcn_s_memrealtime();
@@ -582,21 +579,6 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
             begin(T);
         }
         if (!__any(busy(T) || pend != 0u)) break;
-#if HIPPT_PRIO == 1
-        // issue priority to waves carrying bounced paths over waves of fresh camera rays only
-        if (__ballot(item != kNone && depth > 0)) __builtin_amdgcn_s_setprio(1);
-        else __builtin_amdgcn_s_setprio(0);
-#elif HIPPT_PRIO == 2
-        // by the shallowest bounced path (the most segments possibly left)
-        {
-            const bool b = item != kNone && depth > 0;
-            if (__ballot(b && depth <= 2)) __builtin_amdgcn_s_setprio(3);
-            else if (__ballot(b && depth <= 4)) __builtin_amdgcn_s_setprio(2);
-            else if (__ballot(b)) __builtin_amdgcn_s_setprio(1);
-            else __builtin_amdgcn_s_setprio(0);
-        }
-#endif
-
 
         // ---- traversal: while-while over the BVH; leave once few lanes remain -------------
         if (!CAP || __any(busy(T))) do {

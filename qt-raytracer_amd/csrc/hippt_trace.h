@@ -147,7 +147,7 @@ __device__ __forceinline__ unsigned wave_fetch(bool req, unsigned &poolNext, uns
 // chunks come from its home queue's counter, chunks shrink to kTailChunk items once the queue
 // is within one chunk per wave of its end (a short tail), and a wave whose home queue is
 // drained moves on to the others.  Counters start at 0 and count dynamically claimed items.
-// (Claiming exactly the requesting lanes' count in the tail instead: neutral)
+// (Claiming exactly the requesting lanes' count in the tail instead: neutral, DESIGN_LOG.md §A.1.)
 constexpr unsigned kQueues = kMeshQueues, kQueueStride = 32, kTailChunk = 64;
 
 struct WorkQueue {
@@ -841,7 +841,7 @@ __device__ __forceinline__ void cas_key(unsigned &ka, unsigned &kb) {
 // HYBRID (with QUANT and TOP; bvh_builder.h hybrid_bvh4): the top is 128-byte float nodes (read
 // from LDS, no decode) and every node below it a 64-byte 8-bit node in global memory (4 loads
 // instead of 7 where the TA binds); a node byte offset below topBytes is a top node.  Measured and
-// kept off: the wave's lanes straddle the top/bottom boundary on most iterations,
+// kept off (DESIGN_LOG.md §A.1): the wave's lanes straddle the top/bottom boundary on most iterations,
 // which then run both paths (blob70k 17.5 vs 20.9 G); visiting the top first, the lanes below it
 // waiting, was worse still (11.7 G).
 // PACKED (LDS-resident scenes): packed child keys (pack_key), refBits low bits carrying the code.

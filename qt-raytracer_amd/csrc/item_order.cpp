@@ -179,19 +179,33 @@ void build_item_table(const std::vector<float> &cost, unsigned bandPixels, unsig
     if (!slots) return;
     const unsigned long long total = (unsigned long long)bandPixels * frames;
     auto item = [&](size_t s) { return uint32_t((s / runs) * bandPixels + 64 * (s % runs)); };
-    // per queue (the queue holding a slot's first item): its slots, longest estimate first
-    size_t s = 0;
-    std::vector<size_t> pos, sorted;
-    for (unsigned g = 0; g < queues && s < slots; ++g) {
+    // A stable sort of each queue's slots (s = f*runs + r, ascending) by cost[r], longest first, in
+    // O(slots): the runs by (cost descending, r ascending) once; a queue then takes each group of
+    // equal-cost runs frame by frame (ascending slot order within a group is frame-major).
+    std::vector<uint32_t> ranked(runs);
+    for (size_t r = 0; r < runs; ++r) ranked[r] = uint32_t(r);
+    std::stable_sort(ranked.begin(), ranked.end(), [&](uint32_t a, uint32_t b) { return cost[a] > cost[b]; });
+    std::vector<size_t> group{0};  // group k: ranked[group[k] .. group[k+1])
+    for (size_t k = 1; k < runs; ++k)
+        if (cost[ranked[k]] != cost[ranked[k - 1]]) group.push_back(k);
+    group.push_back(runs);
+    size_t s0 = 0;
+    for (unsigned g = 0; g < queues && s0 < slots; ++g) {
         const unsigned long long end = total * (g + 1) / queues;
-        pos.clear();
-        for (; s < slots && item(s) < end; ++s) pos.push_back(s);
-        sorted = pos;
-        std::stable_sort(sorted.begin(), sorted.end(),
-                         [&](size_t a, size_t b) { return cost[a % runs] > cost[b % runs]; });
-        for (size_t k = 0; k < pos.size(); ++k) table[pos[k]] = item(sorted[k]);
+        size_t s1 = s0;
+        while (s1 < slots && item(s1) < end) ++s1;  // the queue's slots [s0, s1)
+        if (s1 == s0) continue;
+        const size_t f0 = s0 / runs, f1 = (s1 - 1) / runs;
+        size_t out = s0;
+        for (size_t k = 0; k + 1 < group.size(); ++k)
+            for (size_t f = f0; f <= f1; ++f)
+                for (size_t q = group[k]; q < group[k + 1]; ++q) {
+                    const size_t sl = f * runs + ranked[q];
+                    if (sl >= s0 && sl < s1) table[out++] = item(sl);
+                }
+        s0 = s1;
     }
-    for (; s < slots; ++s) table[s] = item(s);
+    for (; s0 < slots; ++s0) table[s0] = item(s0);
 }
 
 }  // namespace hippt

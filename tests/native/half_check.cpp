@@ -72,7 +72,7 @@ int main() {
                 in[k * 32 + 24 + i] = uint32_t(k * 1000 + i - 2);
             }
     std::vector<uint32_t> out;
-    hippt::half_bvh4(in.data(), 2, out);
+    CHECK(hippt::half_bvh4(in.data(), 2, out), "in range");
     CHECK(out.size() == in.size(), "size");
     for (int k = 0; k < 2; ++k) {
         const unsigned char *n = reinterpret_cast<const unsigned char *>(out.data() + k * 32);
@@ -93,6 +93,29 @@ int main() {
         std::memcpy(codes, n + 96, 16);
         for (int i = 0; i < 4; ++i) CHECK(codes[i] == uint32_t(k * 1000 + i - 2), "code");
         for (int b = 112; b < 128; ++b) CHECK(n[b] == 0, "pad");
+    }
+    // empty slots (lo = +inf, hi = -inf) stay infinite; a finite plane beyond the half range means no
+    // half tree (it would become an infinite box)
+    {
+        std::vector<uint32_t> e = in, o;
+        const float pinf = INFINITY, ninf = -INFINITY;
+        for (int a = 0; a < 3; ++a) {
+            std::memcpy(&e[8 * a + 3], &pinf, 4);
+            std::memcpy(&e[8 * a + 4 + 3], &ninf, 4);
+        }
+        CHECK(hippt::half_bvh4(e.data(), 2, o) && o.size() == e.size(), "empty slots");
+        const uint16_t *h = reinterpret_cast<const uint16_t *>(o.data());
+        CHECK(h[3] == 0x7C00u && h[7] == 0xFC00u, "empty slot planes");
+        for (float bad : {70000.0f, -70000.0f}) {
+            std::vector<uint32_t> f = in;
+            std::memcpy(&f[32 + 8 * 2 + (bad > 0 ? 4 : 0) + 1], &bad, 4);  // node 1, axis z, child 1
+            CHECK(!hippt::half_bvh4(f.data(), 2, o) && o.empty(), "beyond the half range");
+        }
+        const float edge = 65504.0f, nedge = -65504.0f;
+        std::vector<uint32_t> g = in;
+        std::memcpy(&g[4], &edge, 4);
+        std::memcpy(&g[0], &nedge, 4);
+        CHECK(hippt::half_bvh4(g.data(), 2, o), "the largest half itself");
     }
     if (fails) return 1;
     std::printf("ok\n");

@@ -530,6 +530,7 @@ def test_item_order_camera_change_does_not_stall(pt):
     pt.uploadMesh(sc2)
     assert pt.initialize(ws, hs), pt.lastError()
     for _ in range(20):  # the first calls in image order, later ones (the estimate done) in cost order
+        assert pt.resetAccumulation()
         assert pt.renderFrames(3, 8), pt.lastError()
         got = pt.readback()
         _assert_same(got[0], got[1], ora[0], ora[1])
@@ -863,13 +864,42 @@ def test_quantized_tree_far_from_origin(pt, offset):
     w, h = 48, 32
     ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
     pt.setOption(hippt.OPT_LDS_SCENE, 0)
-    for width, quant in ((4, 1), (4, 2), (4, 0), (2, -1)):
+    for width, quant in ((4, 1), (4, 2), (4, 3), (4, 0), (2, -1)):
         pt.setOption(hippt.OPT_BVH_WIDTH, width)
         pt.setOption(hippt.OPT_BVH_QUANT, quant)
         assert pt.initialize(w, h)
         assert pt.renderFrames(3, 8)
         got = pt.readback()
         _assert_same(got[0], got[1], ora[0], ora[1])
+
+
+def test_half_tree_beyond_half_range_keeps_float_nodes(pt):
+    """a scene whose planes leave the half range (|x| > 65504) has no half-precision tree:
+    HIPPT_OPT_BVH_QUANT 3 then renders with float nodes (not with boxes widened to infinity, which
+    every ray enters), bit-exact against the oracle and as fast as the float tree."""
+    import dataclasses
+    base = scenes.blob_scene(64, 34, "blob_small")
+    off = np.asarray((9.0e4, 0.0, -7.0e4), np.float32)
+    sc = dataclasses.replace(base, verts=(base.verts.reshape(-1, 3, 3) + off).reshape(-1, 9).astype(np.float32),
+                             lookfrom=tuple(np.asarray(base.lookfrom, np.float32) + off),
+                             lookat=tuple(np.asarray(base.lookat, np.float32) + off))
+    pt.uploadMesh(sc)
+    w, h = 48, 32
+    ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
+    pt.setOption(hippt.OPT_LDS_SCENE, 0)
+    pt.setOption(hippt.OPT_BVH_WIDTH, 4)
+    visits = {}
+    for quant in (3, 0):
+        pt.setOption(hippt.OPT_BVH_QUANT, quant)
+        pt.setOption(hippt.OPT_COUNT_TRAVERSAL, 1)
+        assert pt.initialize(w, h)
+        pt.resetStats()
+        assert pt.renderFrames(3, 8)
+        got = pt.readback()
+        _assert_same(got[0], got[1], ora[0], ora[1])
+        visits[quant] = pt.stats()["nodeVisits"]
+    pt.setOption(hippt.OPT_COUNT_TRAVERSAL, 0)
+    assert visits[3] == visits[0]  # the same (float) tree traversed
 
 
 def test_quantized_tree_tiny_far_nodes(pt):
@@ -892,7 +922,7 @@ def test_quantized_tree_tiny_far_nodes(pt):
     ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
     assert 0 < np.count_nonzero(ora[0] != ora[0][0, 0])  # the cluster is in the picture
     pt.setOption(hippt.OPT_LDS_SCENE, 0)
-    for width, quant in ((4, 1), (4, 2), (4, 0), (2, -1)):
+    for width, quant in ((4, 1), (4, 2), (4, 3), (4, 0), (2, -1)):
         pt.setOption(hippt.OPT_BVH_WIDTH, width)
         pt.setOption(hippt.OPT_BVH_QUANT, quant)
         assert pt.initialize(w, h)
