@@ -240,11 +240,6 @@ enum {
                                        the host's tree), longest first, so that a wave's lanes hold samples
                                        of similar length (1), or in image order (0); -1 (default): automatic
                                        (on).  Same results either way */
-    , HIPPT_OPT_DRAIN_EXPORT = 29   /* megakernel: once the work queues are drained, a wave holding at most this
-                                       many live paths hands them to a second, small launch of the same batch
-                                       (the tail launch) and leaves, so that the launch's last paths run in
-                                       full waves; 0: off; -1 (default): automatic.  Same results either way */
-    , HIPPT_OPT_TAIL_BLOCKS_PER_CU = 30 /* the tail launch's resident blocks per CU (0 = automatic) */
 };
 /* Output frame word formats (HIPPT_OPT_PIXEL_FORMAT).  Both map an accumulated colour c to
  * sqrt(clamp(c, 0, 1)) per channel.

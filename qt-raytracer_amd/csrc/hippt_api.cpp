@@ -56,16 +56,10 @@ constexpr int kSpillStackCap = 10;
 // of the node array is the top of the tree; trees read from global memory keep such a prefix in
 // LDS (HIPPT_OPT_LDS_TOP_NODES)
 constexpr int kTopOrderNodes = 1365;  // 6 complete levels
-// drain export defaults (HIPPT_OPT_DRAIN_EXPORT, HIPPT_OPT_TAIL_BLOCKS_PER_CU)
-constexpr int kDrainExportAuto = 0;
-constexpr int kTailBlocksPerCuAuto = 2;
 // hippt_trace.h kQueues x kQueueStride work counters, then (its own line) the fused combine's
 // chunk counter (MeshParams::combCtr)
 constexpr size_t kCombCtrWord = 8 * 32;
-// then the drain export's record count and the tail launch's claim counter (MeshParams::exportCtr,
-// exportClaim), each on its own line
-constexpr size_t kExportCtrWord = kCombCtrWord + 32, kExportClaimWord = kCombCtrWord + 64;
-constexpr size_t kQueueBytes = (kCombCtrWord + 96) * sizeof(unsigned);
+constexpr size_t kQueueBytes = (kCombCtrWord + 32) * sizeof(unsigned);
 
 struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
@@ -150,10 +144,6 @@ struct Ctx {
     std::shared_ptr<CostJob> costJob;  // automatic mode: the costs of a new key, off the render path
     int *spill = nullptr;      // 4-wide traversal: per-lane stack spill area
     size_t spillBytes = 0;
-    float4 *exportBuf = nullptr;  // drain export records (MeshParams::exportBuf), one per lane of the grid
-    size_t exportBytes = 0;
-    long long tailOccKey = -1;  // tail-launch occupancy cached like occKey
-    int tailBlocksPerCu = 0;
     // wavefront path-state pool (allocated on first use)
     void *wfPool = nullptr;
     unsigned wfSlots = 0;  // slots allocated
@@ -231,8 +221,6 @@ struct State {
     int cameraPool = -1;  // megakernel camera-ray pool (HIPPT_OPT_CAMERA_POOL; -1: automatic)
     int fuseCombine = -1;  // combine inside the next megakernel launch (HIPPT_OPT_FUSE_COMBINE)
     int itemOrder = -1;    // scene-hitting pixel runs first (HIPPT_OPT_ITEM_ORDER; -1: automatic)
-    int drainExport = -1;  // live-path threshold of the drain export (HIPPT_OPT_DRAIN_EXPORT; -1: automatic)
-    int tailBlocksPerCu = 0;  // the tail launch's grid (HIPPT_OPT_TAIL_BLOCKS_PER_CU; 0: automatic)
     std::vector<std::pair<int, uint32_t *>> rngTables;  // per device, built on first use
     unsigned activeTopBytes = 0;  // of the last mesh render (hipptGetOption HIPPT_INFO_*)
     int activeBlocksPerCu = 0;
@@ -405,9 +393,6 @@ void destroy_ctx(Ctx &c) {
     (void)hipFree(c.spill);
     c.spill = nullptr;
     c.spillBytes = 0;
-    (void)hipFree(c.exportBuf);
-    c.exportBuf = nullptr;
-    c.exportBytes = 0;
     (void)hipHostFree(c.wfHost);
     for (hipEvent_t e : c.wfPoll)
         if (e) (void)hipEventDestroy(e);
@@ -748,19 +733,6 @@ bool ensure_spill(Ctx &c, hippt::MeshParams &p, long long blocks, bool spills, i
         c.spillBytes = bytes;
     }
     p.spill = c.spill;
-    return true;
-}
-
-// The drain export's record buffer for `lanes` lanes of a persistent grid (one record each at most).
-bool ensure_export(Ctx &c, size_t lanes, const char **err) {
-    const size_t bytes = lanes * hippt::kExportF4 * sizeof(float4);
-    if (c.exportBytes >= bytes) return true;
-    HIP_TRY(hipStreamSynchronize(c.stream));
-    (void)hipFree(c.exportBuf);
-    c.exportBuf = nullptr;
-    c.exportBytes = 0;
-    HIP_TRY(hipMalloc(&c.exportBuf, bytes));
-    c.exportBytes = bytes;
     return true;
 }
 
@@ -1205,42 +1177,10 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                                 c.hasDeferred = false;
                             }
                             p.combCtr = c.queue + kCombCtrWord;
-                            // Drain export (not in counting launches: the tail kernels are the timed
-                            // variants)
-                            const int thr = cnt ? 0 : s.drainExport >= 0 ? s.drainExport : kDrainExportAuto;
-                            long long tailBlocks = 0;
-                            if (thr > 0) {
-                                if (!ensure_export(c, size_t(blocks) * hippt::kMeshBlock, err)) return false;
-                                const long long tk = occKey ^ (long long)(spills ? 1 : 0) << 50;
-                                if (c.tailOccKey != tk) {
-                                    const int ln = ldsScene ? numNodes : 0, lt = ldsScene ? numTris : 0,
-                                              lm = ldsScene ? numMats : 0;
-                                    c.tailBlocksPerCu = hippt::mesh_tail_blocks_per_cu(s.scene.full, fmt, stackDepth, ln,
-                                                                                       lt, spills, topBytes, lm);
-                                    c.tailOccKey = tk;
-                                }
-                                const int tbpc = s.tailBlocksPerCu > 0 ? std::min(s.tailBlocksPerCu, c.tailBlocksPerCu)
-                                                                       : std::min(kTailBlocksPerCuAuto, c.tailBlocksPerCu);
-                                tailBlocks = std::min<long long>(blocks, (long long)c.cus * tbpc);
-                                p.exportBuf = c.exportBuf;
-                                p.exportCtr = c.queue + kExportCtrWord;
-                                p.exportClaim = c.queue + kExportClaimWord;
-                                p.exportThr = unsigned(thr);
-                            }
                             EventPair ev;
                             if (!next_events(c, ev, err)) return false;
                             HIP_TRY(hipEventRecord(ev.a, c.stream));
                             HIP_TRY(hippt::launch_mesh(p, int(blocks), cnt, c.stream));
-                            if (thr > 0) {
-                                // the tail launch: the exported paths in full waves
-                                hippt::MeshParams t = p;
-                                t.tailMode = 1;
-                                t.poolWords = 0;
-                                t.poolOffset = 0;
-                                t.comb = hippt::CombineParams{};
-                                t.exportThr = 0;
-                                HIP_TRY(hippt::launch_mesh_tail(t, int(tailBlocks), c.stream));
-                            }
                             HIP_TRY(hipEventRecord(ev.b, c.stream));
                             c.pending.push_back({0, ev});
                         }
@@ -1965,14 +1905,6 @@ extern "C" bool hipptSetOption(int key, long long value) try {
         if (value < -1 || value > 1) return false;
         s.itemOrder = int(value);
         return true;
-    case HIPPT_OPT_DRAIN_EXPORT:
-        if (value < -1 || value > 64) return false;
-        s.drainExport = int(value);
-        return true;
-    case HIPPT_OPT_TAIL_BLOCKS_PER_CU:
-        if (value < 0 || value > 8) return false;
-        s.tailBlocksPerCu = int(value);
-        return true;
     default: return false;
     }
 } catch (const std::exception &e) {
@@ -2021,8 +1953,6 @@ extern "C" long long hipptGetOption(int key) try {
     case HIPPT_OPT_CAMERA_POOL: return s.cameraPool;
     case HIPPT_OPT_FUSE_COMBINE: return s.fuseCombine;
     case HIPPT_OPT_ITEM_ORDER: return s.itemOrder;
-    case HIPPT_OPT_DRAIN_EXPORT: return s.drainExport;
-    case HIPPT_OPT_TAIL_BLOCKS_PER_CU: return s.tailBlocksPerCu;
     case HIPPT_INFO_LDS_TOP_BYTES: return s.activeTopBytes;
     case HIPPT_INFO_BLOCKS_PER_CU: return s.activeBlocksPerCu;
     default: return -1;

@@ -109,18 +109,7 @@ struct MeshParams {
     // claimed from *combCtr (zeroed with the work queue)
     CombineParams comb;
     unsigned *combCtr;
-    // Drain export (the launch's tail): once a wave has found the queues drained and
-    // holds at most exportThr live paths (0: never), it appends them to exportBuf (kExportF4 float4
-    // per path: (o.xyz, d.x) (d.yz, throughput.rg) (throughput.b, rng, depth, item)) at
-    // *exportCtr and leaves; a tail launch (tailMode 1, same scene and batch) then takes the
-    // records instead of work items, claiming them at *exportClaim, with full lanes.
-    float4 *exportBuf;
-    unsigned *exportCtr;
-    unsigned *exportClaim;
-    unsigned exportThr;
-    int tailMode;
 };
-constexpr int kExportF4 = 3;
 
 
 // MeshParams::wide
@@ -141,10 +130,6 @@ inline hipError_t check_lds_at_zero(const void *kernel) {
 
 hipError_t launch_sphere4(const Sphere4Params &p, hipStream_t s);
 hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hipStream_t s);
-// The tail launch of a drain export (MeshParams::tailMode): p as for the batch's launch_mesh.
-hipError_t launch_mesh_tail(const MeshParams &p, int blocks, hipStream_t s);
-int mesh_tail_blocks_per_cu(bool full, int fmt, int stackDepth, int ldsNodes, int ldsTris, bool spill, unsigned topBytes,
-                            int ldsMats);
 hipError_t launch_combine(const CombineParams &p, hipStream_t s, const HostFrame &h = HostFrame{});
 // random_in_unit_sphere's rejection loop (RayTracer.h:155-161 with the hash RNG and the short-cycle
 // escape) is a pure function of the RNG state it starts from: table[s] = the state from which the

@@ -286,31 +286,10 @@ __device__ __forceinline__ void pool_take(const MeshParams &P, const float *pool
     }
 }
 
-// A drained wave's live paths into the export buffer (MeshParams::exportBuf), one record per lane
-// holding a sample; a path in mid-traversal restarts its traversal in the tail launch (the closest
-// hit is argmin (t, primitive id): no result bit depends on the traversal's history).
-__device__ __forceinline__ void export_paths(const MeshParams &P, unsigned item, const Ray &r, float tr, float tg,
-                                             float tb, uint32_t rng, int depth) {
-    const bool live = item != kNone;
-    const unsigned long long m = __ballot(live);
-    if (!m) return;
-    const unsigned rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
-    unsigned base = 0;
-    if (__lane_id() == 0) base = atomicAdd(P.exportCtr, unsigned(__popcll(m)));
-    base = __builtin_amdgcn_readfirstlane(base);
-    if (live) {
-        float4 *rec = P.exportBuf + size_t(base + rank) * kExportF4;
-        rec[0] = make_float4(r.ox, r.oy, r.oz, r.dx);
-        rec[1] = make_float4(r.dy, r.dz, tr, tg);
-        rec[2] = make_float4(tb, __uint_as_float(rng), __int_as_float(depth), __uint_as_float(item));
-    }
-}
-
 template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE, bool QUANT, bool SPILL = true, bool POOL = false,
-          bool HYBRID = false, bool HALF = false, bool TAIL = false>
+          bool HYBRID = false, bool HALF = false>
 __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_EU : HIPPT_MESH_WAVES_PER_EU) HIPPT_SGPR_ATTR void mesh_kernel(MeshParams P) {
     static_assert(!QUANT || (WIDE && !LDS_SCENE), "quantized nodes: 4-wide global-memory traversal only");
-    static_assert(!TAIL || !POOL, "the tail launch takes export records, not camera rays");
 #ifdef HIPPT_DEBUG_TIMELINE
     const unsigned tlw = blockIdx.x * 4u + (threadIdx.x >> 6);
     unsigned long long tlDrained = 0, tlItems = 0, tlRounds = 0, tlLate = 0;
@@ -440,9 +419,6 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     };
 #endif
     unsigned waveThr = unsigned(P.waveThreshold);
-    // the wave found the queues drained (drain export) / the tail launch's records (TAIL)
-    bool drained = false;
-    const unsigned tailTotal = TAIL ? __builtin_amdgcn_readfirstlane(*reinterpret_cast<volatile unsigned *>(P.exportCtr)) : 0u;
     bool combLeft = P.comb.bandPixels != 0;
     if (combLeft && (blockIdx.x & 1u) == 0 && threadIdx.x < 64u)
         while (combLeft) combLeft = combine_chunk(P);
@@ -508,44 +484,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                     depth = 0;
                     fresh = true;
                 }
-                if (__ballot(took && item == kNone)) {
-                    drained = true;
-                    if (FINISH) waveThr = 0u;
-                }
-            }
-        } else if (TAIL) {
-            // the tail launch: the next export records for the lanes whose paths ended
-            const unsigned long long m = __ballot(need);
-            if (m) {
-                const unsigned rank =
-                    __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
-                unsigned base = 0;
-                if (__lane_id() == 0) base = atomicAdd(P.exportClaim, unsigned(__popcll(m)));
-                base = __builtin_amdgcn_readfirstlane(base);
-                const unsigned k = base + rank;
-                if (need) {
-                    need = false;
-                    item = kNone;
-                    if (k < tailTotal) {
-                        const float4 *rec = P.exportBuf + size_t(k) * kExportF4;
-                        const float4 a = rec[0], b = rec[1], c = rec[2];
-                        r.ox = a.x;
-                        r.oy = a.y;
-                        r.oz = a.z;
-                        r.dx = a.w;
-                        r.dy = b.x;
-                        r.dz = b.y;
-                        tr = b.z;
-                        tg = b.w;
-                        tb = c.x;
-                        rng = __float_as_uint(c.y);
-                        depth = __float_as_int(c.z);
-                        item = __float_as_uint(c.w);
-                        fresh = true;
-                    }
-                }
-                // records drained: traversals run to the end (no lane can be refilled)
-                if (base + unsigned(__popcll(m)) >= tailTotal) waveThr = 0u;
+                if (FINISH && __ballot(took && item == kNone)) waveThr = 0u;
             }
         } else if (__ballot(need)) {
             const unsigned it = order_item(P, queue_fetch(need, Q, P.queue, P.totalItems, P.chunk));
@@ -553,7 +492,6 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
             if (!tlDrained && __ballot(need && it == kNone)) tlDrained = __builtin_amdgcn_s_memrealtime();
             tlItems += __popcll(__ballot(it != kNone));
 #endif
-            if (__ballot(need && it == kNone)) drained = true;
             if (need) {
                 need = false;
                 item = it;
@@ -565,11 +503,6 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                     fresh = true;
                 }
             }
-        }
-        // drain export: a drained wave with few live paths hands them to the tail launch and leaves
-        if (!TAIL && P.exportThr && drained && unsigned(__popcll(__ballot(item != kNone))) <= P.exportThr) {
-            export_paths(P, item, r, tr, tg, tb, rng, depth);
-            break;
         }
         // new rays (refilled or scattered): one place, so a pass with lanes of both kinds runs
         // the reciprocals once
@@ -588,7 +521,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                     T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit, S, P.topBytes, P.refBits);
             else
                 traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);
-        } while (__popcll(__ballot(busy(T))) > ((FINISH || TAIL) ? waveThr : unsigned(P.waveThreshold)));
+        } while (__popcll(__ballot(busy(T))) > (FINISH ? waveThr : unsigned(P.waveThreshold)));
 
         // ---- shading: lanes whose traversal finished (ray_color step, RayTracer.h:579-596) ----
         if (item != kNone && !busy(T)) {
@@ -824,51 +757,6 @@ hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hip
     }
     hipLaunchKernelGGL(fn, dim3(blocks), dim3(kMeshBlock), bytes, s, p);
     return hipGetLastError();
-}
-
-// The tail launch's kernels: the timed (non-counting) variants without the camera-ray pool.
-static MeshFn mesh_fn_tail(bool lds, bool full, int fmt, bool spill) {
-#define HIPPT_TAIL_FN(FULL_, SPILL_)                                                                              \
-    (lds ? (fmt == kWide2 ? mesh_kernel<false, true, FULL_, false, false, SPILL_, false, false, false, true>        \
-                          : mesh_kernel<false, true, FULL_, true, false, SPILL_, false, false, false, true>)       \
-     : fmt == kWide2       ? mesh_kernel<false, false, FULL_, false, false, SPILL_, false, false, false, true>      \
-     : fmt == kWideQuant   ? mesh_kernel<false, false, FULL_, true, true, SPILL_, false, false, false, true>       \
-     : fmt == kWideHybrid  ? mesh_kernel<false, false, FULL_, true, true, SPILL_, false, true, false, true>        \
-     : fmt == kWideHalf    ? mesh_kernel<false, false, FULL_, true, false, SPILL_, false, false, true, true>       \
-                           : mesh_kernel<false, false, FULL_, true, false, SPILL_, false, false, false, true>)
-    // 2-wide trees have no stack cap: their kernels keep the spill code path (SPILL = true)
-    if (full) return spill || fmt == kWide2 ? HIPPT_TAIL_FN(true, true) : HIPPT_TAIL_FN(true, false);
-    return spill || fmt == kWide2 ? HIPPT_TAIL_FN(false, true) : HIPPT_TAIL_FN(false, false);
-#undef HIPPT_TAIL_FN
-}
-
-hipError_t launch_mesh_tail(const MeshParams &p, int blocks, hipStream_t s) {
-    if (!p.tailMode || !p.exportBuf || !p.exportCtr || !p.exportClaim || p.poolWords || p.comb.bandPixels)
-        return hipErrorInvalidValue;
-    if (p.stackDepth < 1 || p.stackDepth > kStackDepth) return hipErrorInvalidValue;
-    if (p.wide && (p.stackCap < 1 || p.stackCap + 2 > p.stackDepth)) return hipErrorInvalidValue;
-    const bool lds = p.ldsScene != 0;
-    if (p.wide < kWide2 || p.wide > kWideHalf || (lds && p.wide >= kWideQuant)) return hipErrorInvalidValue;
-    const size_t bytes = mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0, p.wide != 0, p.topBytes,
-                                        lds ? p.numMats : 0, 0);
-    const MeshFn fn = mesh_fn_tail(lds, p.full != 0, p.wide, p.spill != nullptr);
-    if (p.wide && (lds || p.topBytes)) {
-        const hipError_t e = check_lds_at_zero(reinterpret_cast<const void *>(fn));
-        if (e != hipSuccess) return e;
-    }
-    hipLaunchKernelGGL(fn, dim3(blocks), dim3(kMeshBlock), bytes, s, p);
-    return hipGetLastError();
-}
-
-int mesh_tail_blocks_per_cu(bool full, int fmt, int stackDepth, int ldsNodes, int ldsTris, bool spill, unsigned topBytes,
-                            int ldsMats) {
-    int n = 0;
-    const bool lds = ldsNodes > 0;
-    const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, fmt != kWide2, topBytes, ldsMats, 0);
-    const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &n, mesh_fn_tail(lds, full, lds && fmt >= kWideQuant ? kWideFloat : fmt, spill), kMeshBlock, bytes);
-    if (e != hipSuccess || n <= 0) n = 1;
-    return std::min(n, kMaxResidentBlocks);
 }
 
 hipError_t launch_combine(const CombineParams &p, hipStream_t s, const HostFrame &h) {

@@ -92,8 +92,6 @@ def test_options_validate():
     (hippt.OPT_ITEM_ORDER, (-1, 0, 1), (-2, 2), -1),
     (hippt.OPT_STACK_CAP, (0, 4, 30), (3, 31), 0),
     (hippt.OPT_BVH_QUANT, (-1, 0, 1, 2, 3), (-2, 4), -1),
-    (hippt.OPT_DRAIN_EXPORT, (-1, 0, 16, 64), (-2, 65), -1),
-    (hippt.OPT_TAIL_BLOCKS_PER_CU, (0, 1, 8), (-1, 9), 0),
 ])
 def test_round2_options_round_trip(key, good, bad, default):
     """Each option accepts its documented range (include/hippt.h), reads back what was set,

@@ -30,8 +30,7 @@ def pt():
                  (hippt.OPT_STACK_CAP, 0), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_LDS_TOP_NODES, -1),
                  (hippt.OPT_RNG_TABLE, 0), (hippt.OPT_BVH_COLLAPSE, -1), (hippt.OPT_BVH_NODE_COST, 200),
                  (hippt.OPT_BVH_LEAF4, 4), (hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_ARGB),
-                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1), (hippt.OPT_ITEM_ORDER, -1),
-                 (hippt.OPT_DRAIN_EXPORT, -1), (hippt.OPT_TAIL_BLOCKS_PER_CU, 0)):
+                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1), (hippt.OPT_ITEM_ORDER, -1)):
         t.setOption(k, v)
     t.resetStats()
     yield t
@@ -535,29 +534,6 @@ def test_item_order_camera_change_does_not_stall(pt):
         got = pt.readback()
         _assert_same(got[0], got[1], ora[0], ora[1])
         time.sleep(0.005)
-
-
-@pytest.mark.parametrize("name,w,h,frames", [("cornell34", 200, 77, 3), ("blob70k", 131, 64, 2),
-                                               ("cornell_mixed", 96, 53, 2), ("random_scene", 77, 41, 2)])
-def test_drain_export_does_not_change_results(pt, name, w, h, frames):
-    """HIPPT_OPT_DRAIN_EXPORT: drained waves with at most N live paths hand them (ray, throughput, RNG
-    state, depth, item) to a second, small launch of the same batch, which finishes them with full
-    lanes; the image and the counts are the oracle's for every threshold (64: every drained wave
-    exports) and tail-launch size, with the camera pool on and off."""
-    sc = scenes.get_scene(name)
-    ora = po.MeshScene(sc, w, h).frames(0, frames, 8)
-    pt.uploadMesh(sc)
-    for thr, bpc, pool in ((64, 1, -1), (16, 0, -1), (32, 8, 0), (64, 2, 0)):
-        pt.setOption(hippt.OPT_DRAIN_EXPORT, thr)
-        pt.setOption(hippt.OPT_TAIL_BLOCKS_PER_CU, bpc)
-        pt.setOption(hippt.OPT_CAMERA_POOL, pool)
-        assert pt.initialize(w, h), pt.lastError()
-        assert pt.renderFrames(frames, 8), pt.lastError()
-        got = pt.readback()
-        _assert_same(got[0], got[1], ora[0], ora[1])
-        st = pt.stats()
-        assert st["segments"] == ora[2] and st["pixelSamples"] == ora[3]
-        pt.resetStats()
 
 
 @pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene"])
