@@ -240,6 +240,10 @@ enum {
                                        the host's tree), longest first, so that a wave's lanes hold samples
                                        of similar length (1), or in image order (0); -1 (default): automatic
                                        (on).  Same results either way */
+    , HIPPT_OPT_WAVEFRONT_SORT = 29 /* wavefront: the shade kernel appends each block's scattered paths sorted by
+                                       direction octant (3) or octant and a 2x2x2 cell of the scene box (6),
+                                       so that a wave of the extend kernel traces rays of one kind; 0: in
+                                       thread order; -1 (default): automatic (0).  Same results either way */
 };
 /* Output frame word formats (HIPPT_OPT_PIXEL_FORMAT).  Both map an accumulated colour c to
  * sqrt(clamp(c, 0, 1)) per channel.

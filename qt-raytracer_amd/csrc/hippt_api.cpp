@@ -231,6 +231,7 @@ struct State {
     // wavefront path-state slots per device: 2^27 holds a whole 1080p/64-spp step in flight (one
     // generation, no regenerate rounds; 8.6 GB of 64-byte records): blob70k 6.8 -> 7.4+ G vs 2^24
     unsigned wfSlots = 1u << 27;
+    int wfSort = -1;  // wavefront coherence sort key bits (HIPPT_OPT_WAVEFRONT_SORT: 0, 3, 6; -1 automatic)
     hippt::BvhParams bvh;         // applied at the next scene upload
     // host-side timing accumulators
     double traceMs = 0, combineMs = 0;
@@ -808,6 +809,27 @@ bool run_wavefront(Ctx &c, hippt::MeshParams p, bool cnt, bool spills, int spill
         W.rc[q] = base + (3 * q + 2) * entries;
     }
     W.hit = reinterpret_cast<float2 *>(base + 6 * entries);
+    // coherence sort of the scattered paths (HIPPT_OPT_WAVEFRONT_SORT; automatic: off)
+    W.sortBits = unsigned(s.wfSort > 0 ? s.wfSort : 0);
+    if (W.sortBits > 3) {
+        // the scene box: the union of the 4-wide root's child boxes (Bvh4 words lo.x[4] hi.x[4] ...)
+        const std::vector<uint32_t> &n = s.scene.bvh4.nodes;
+        for (int a = 0; a < 3; ++a) {
+            float lo = INFINITY, hi = -INFINITY;
+            for (int i = 0; i < 4 && n.size() >= size_t(hippt::kNode4Words); ++i) {
+                float l, h;
+                std::memcpy(&l, &n[size_t(8 * a + i)], 4);
+                std::memcpy(&h, &n[size_t(8 * a + 4 + i)], 4);
+                if (l <= h) {
+                    lo = std::min(lo, l);
+                    hi = std::max(hi, h);
+                }
+            }
+            const bool ok = std::isfinite(lo) && std::isfinite(hi) && hi > lo;
+            W.sortLo[a] = ok ? lo : 0.0f;
+            W.sortScale[a] = ok ? 2.0f / (hi - lo) : 0.0f;
+        }
+    }
     const bool wide = p.wide != 0, quant = p.wide == 2;
     const long long occKey = occupancy_key(s.scene.version, p.stackDepth, p.ldsScene != 0, p.full != 0, wide, quant) ^
                              ((long long)p.topBytes << 40) ^ ((long long)(p.wide == hippt::kWideHalf) << 34);
@@ -1905,6 +1927,10 @@ extern "C" bool hipptSetOption(int key, long long value) try {
         if (value < -1 || value > 1) return false;
         s.itemOrder = int(value);
         return true;
+    case HIPPT_OPT_WAVEFRONT_SORT:
+        if (value != -1 && value != 0 && value != 3 && value != 6) return false;
+        s.wfSort = int(value);
+        return true;
     default: return false;
     }
 } catch (const std::exception &e) {
@@ -1953,6 +1979,7 @@ extern "C" long long hipptGetOption(int key) try {
     case HIPPT_OPT_CAMERA_POOL: return s.cameraPool;
     case HIPPT_OPT_FUSE_COMBINE: return s.fuseCombine;
     case HIPPT_OPT_ITEM_ORDER: return s.itemOrder;
+    case HIPPT_OPT_WAVEFRONT_SORT: return s.wfSort;
     case HIPPT_INFO_LDS_TOP_BYTES: return s.activeTopBytes;
     case HIPPT_INFO_BLOCKS_PER_CU: return s.activeBlocksPerCu;
     default: return -1;

@@ -148,7 +148,10 @@ __device__ __forceinline__ unsigned wave_fetch(bool req, unsigned &poolNext, uns
 // is within one chunk per wave of its end (a short tail), and a wave whose home queue is
 // drained moves on to the others.  Counters start at 0 and count dynamically claimed items.
 // (Claiming exactly the requesting lanes' count in the tail instead: neutral, DESIGN_LOG.md §A.1.)
-constexpr unsigned kQueues = kMeshQueues, kQueueStride = 32, kTailChunk = 64;
+#ifndef HIPPT_TAIL_CHUNK
+#define HIPPT_TAIL_CHUNK 64
+#endif
+constexpr unsigned kQueues = kMeshQueues, kQueueStride = 32, kTailChunk = HIPPT_TAIL_CHUNK;
 
 struct WorkQueue {
     unsigned g, left;  // current queue, queues not yet found drained

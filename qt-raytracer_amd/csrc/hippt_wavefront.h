@@ -39,6 +39,12 @@ struct WfParams {
     float2 *hit;
     unsigned *ctr;
     unsigned slots, shardCap;
+    // Coherence sort of the scattered paths (HIPPT_OPT_WAVEFRONT_SORT): wf_shade appends each
+    // block's paths in the order of a key, so that a wave of wf_extend takes rays of one direction
+    // octant (sortBits 3) and, with sortBits 6, one cell of a 2x2x2 grid over the scene's box
+    // (cell c on axis a: (o_a - sortLo[a]) * sortScale[a] in [c, c+1)); 0: append in thread order.
+    unsigned sortBits;
+    float sortLo[3], sortScale[3];
 };
 
 // Words of the queues: 2 x 3 float4 + the hit float2 per entry, kWfShards segments of

@@ -73,6 +73,36 @@ __device__ __forceinline__ unsigned block_append(bool req, unsigned cap, unsigne
     return at;
 }
 
+// block_append with the block's appends ordered by key (< 64; WfParams::sortBits): an LDS counting
+// sort, one atomic per block as before.  A path's entry within its key's bin follows the LDS atomics'
+// order: the queue's order changes which lane traces a path, never what it computes.
+__device__ __forceinline__ unsigned block_append_sorted(bool req, unsigned key, unsigned bins, unsigned cap,
+                                                        unsigned *ctr, int q, unsigned *lds) {
+    if (threadIdx.x < 64) lds[threadIdx.x] = 0;
+    __syncthreads();
+    const unsigned rank = req ? atomicAdd(&lds[key], 1u) : 0u;
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        // exclusive scan of the bin counts (wave 0)
+        const unsigned v = threadIdx.x < bins ? lds[threadIdx.x] : 0u;
+        unsigned inc = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const unsigned t = __shfl_up(inc, o);
+            if (int(threadIdx.x) >= o) inc += t;
+        }
+        lds[threadIdx.x] = inc - v;
+        if (threadIdx.x == 63) {
+            const unsigned shard = blockIdx.x % kWfShards;
+            lds[64] = inc ? shard * cap + atomicAdd(&ctr[ctr_word(ctr_queue(q) + int(shard))], inc) : 0u;
+        }
+    }
+    __syncthreads();
+    const unsigned at = req ? lds[64] + lds[key] + rank : kNone;
+    __syncthreads();
+    return at;
+}
+
 // Counters of both queues and the work base start at 0.
 static_assert(kCtrCount <= 64, "wf_init clears the counters with one wave");
 __global__ void wf_init(WfParams W) {
@@ -194,7 +224,8 @@ __global__ __launch_bounds__(kMeshBlock) void wf_extend(WfParams W, int cur) {
 // holds more than its ceil(slots / kWfShards) entries.
 template <bool FULL>
 __global__ __launch_bounds__(kWfBlock) void wf_shade(WfParams W, int cur) {
-    __shared__ unsigned lds[kWfBlock / 64 + 1];
+    static_assert(kWfBlock / 64 + 1 <= 65, "one LDS array serves both appends");
+    __shared__ unsigned lds[65];
     const MeshParams &P = W.mp;
     if (blockIdx.x == 0 && threadIdx.x < kWfShards) W.ctr[ctr_word(kCtrFetch + int(threadIdx.x))] = 0;
     const unsigned shard = blockIdx.x % kWfShards;
@@ -237,7 +268,20 @@ __global__ __launch_bounds__(kWfBlock) void wf_shade(WfParams W, int cur) {
         }
         if (finished) store_radiance(P.scratch, q.item, L0, L1, L2);
     }
-    const unsigned at = block_append(again, W.shardCap, W.ctr, cur ^ 1, lds);
+    unsigned at;
+    if (W.sortBits) {
+        // direction octant, then the origin's cell of a 2x2x2 grid over the scene box
+        unsigned key = (q.r.dx < 0.0f ? 1u : 0u) | (q.r.dy < 0.0f ? 2u : 0u) | (q.r.dz < 0.0f ? 4u : 0u);
+        if (W.sortBits > 3) {
+            const unsigned cx = (q.r.ox - W.sortLo[0]) * W.sortScale[0] >= 1.0f ? 1u : 0u;
+            const unsigned cy = (q.r.oy - W.sortLo[1]) * W.sortScale[1] >= 1.0f ? 1u : 0u;
+            const unsigned cz = (q.r.oz - W.sortLo[2]) * W.sortScale[2] >= 1.0f ? 1u : 0u;
+            key = key << 3 | cx | cy << 1 | cz << 2;
+        }
+        at = block_append_sorted(again, again ? key : 0u, 1u << W.sortBits, W.shardCap, W.ctr, cur ^ 1, lds);
+    } else {
+        at = block_append(again, W.shardCap, W.ctr, cur ^ 1, lds);
+    }
     if (again) store_path(W, cur ^ 1, at, q);
 }
 

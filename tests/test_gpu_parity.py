@@ -30,7 +30,8 @@ def pt():
                  (hippt.OPT_STACK_CAP, 0), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_LDS_TOP_NODES, -1),
                  (hippt.OPT_RNG_TABLE, 0), (hippt.OPT_BVH_COLLAPSE, -1), (hippt.OPT_BVH_NODE_COST, 200),
                  (hippt.OPT_BVH_LEAF4, 4), (hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_ARGB),
-                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1), (hippt.OPT_ITEM_ORDER, -1)):
+                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1), (hippt.OPT_ITEM_ORDER, -1),
+                 (hippt.OPT_WAVEFRONT_SORT, -1)):
         t.setOption(k, v)
     t.resetStats()
     yield t
@@ -154,6 +155,29 @@ def test_wavefront_matches_oracle(pt, name, w, h, spp, depth, slots, width, cap)
     _assert_same(px, acc, ora_px, ora_acc)
     st = pt.stats()
     assert st["segments"] == segs and st["pixelSamples"] == samples
+
+
+@pytest.mark.parametrize("name,w,h", [("cornell34", 96, 54), ("blob70k", 80, 45), ("cornell_mixed", 64, 40),
+                                      ("random_scene", 77, 41)])
+def test_wavefront_sort_does_not_change_results(pt, name, w, h):
+    """HIPPT_OPT_WAVEFRONT_SORT: the shade kernel's appends ordered by direction octant (3) or octant
+    and scene-box cell (6) per block; the image and the counts are the oracle's for every key, with
+    a pool small enough that paths regenerate (slots shared between generations)."""
+    sc = scenes.get_scene(name)
+    ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
+    pt.uploadMesh(sc)
+    pt.setOption(hippt.OPT_PATH_MODE, 1)
+    for slots in (1 << 24, 4096):
+        pt.setOption(hippt.OPT_WAVEFRONT_SLOTS, slots)
+        for key in (3, 6, 0):
+            pt.setOption(hippt.OPT_WAVEFRONT_SORT, key)
+            assert pt.initialize(w, h), pt.lastError()
+            pt.resetStats()
+            assert pt.renderFrames(3, 8), pt.lastError()
+            got = pt.readback()
+            _assert_same(got[0], got[1], ora[0], ora[1])
+            st = pt.stats()
+            assert st["segments"] == ora[2] and st["pixelSamples"] == ora[3]
 
 
 @pytest.mark.parametrize("name", ["blob70k", "random_scene"])
