@@ -243,6 +243,29 @@ def load_pmc(args, workload: str):
     return None
 
 
+# PMC summaries older than this live run, or of another image, are not this run's traffic
+PMC_TIME_TOLERANCE = 0.10
+
+
+def check_pmc(pmc, image_crc, mean_launch_ms: float, world: int):
+    """The PMC summary of this workload only where it describes this run: the same
+    image (the summary's image_crc32 = this run's) and a kernel time within PMC_TIME_TOLERANCE of
+    this run's mean launch.  Otherwise (None, reason): roofline.traffic is null and says why."""
+    if not pmc:
+        return None, None
+    if world > 1:
+        return None, "the PMC summaries are single-GPU profiles of the whole image"
+    if pmc.get("image_crc32") is None:
+        return None, f"{pmc.get('source')}: no image_crc32 recorded (profile predates the check)"
+    if image_crc is not None and int(pmc["image_crc32"]) != int(image_crc):
+        return None, f"{pmc.get('source')}: image CRC {pmc['image_crc32']} is not this run's {image_crc}"
+    prof_ms = pmc.get("mean_launch_ms_rocprof")
+    if not prof_ms or mean_launch_ms <= 0 or abs(prof_ms - mean_launch_ms) > PMC_TIME_TOLERANCE * mean_launch_ms:
+        return None, (f"{pmc.get('source')}: rocprof mean {prof_ms} ms is not within "
+                      f"{PMC_TIME_TOLERANCE:.0%} of this run's {mean_launch_ms:.4f} ms per launch")
+    return pmc, None
+
+
 def make_roofline(args, pmc, traffic, mean_launch_ms, launches, alg_bytes_launch, flops_launch, counted,
                   alg_gbs) -> dict:
     """Roofline of the dominant kernel.  This path is branchy scalar FP32 over a cache-resident
@@ -401,10 +424,8 @@ def main():
     samples = hd.sum_over_ranks(st["pixelSamples"], dist)
     value = segments / elapsed_max / 1e6
 
-    # output image of the last step: gathered bands (untimed), checksum on rank 0
-    px = pt.readback()[0][my_rows]
-    full = (hd.gather_interleaved(px, args.height, dist) if args.split == "interleave"
-            else hd.gather_bands(px, args.height, dist))
+    # output image of the last step: gathered bands (untimed), checksum on rank 0 (below, with the
+    # PMC summary's check)
 
     # roofline of the dominant (mesh) kernel, from this rank's counted pass and live events
     launches = max(1, st["traceLaunches"] // max(1, args.steps))
@@ -422,10 +443,18 @@ def main():
     if args.path_mode == "wavefront":
         workload += " wavefront"
     pmc = load_pmc(args, workload)
+    px = pt.readback()[0][my_rows]
+    full = (hd.gather_interleaved(px, args.height, dist) if args.split == "interleave"
+            else hd.gather_bands(px, args.height, dist))
+    import zlib
+    image_crc = zlib.crc32(full.tobytes()) & 0xFFFFFFFF if full is not None else None
+    pmc, pmc_refused = check_pmc(pmc, image_crc, mean_launch_ms, world)
     traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
 
     roofline = make_roofline(args, pmc, traffic, mean_launch_ms, launches, alg_bytes_launch, flops_launch,
                              counted, achieved)
+    if pmc_refused:
+        roofline["pmc_refused"] = pmc_refused
 
     k = baseline_config_index(args)
     workload_label = workload
@@ -434,7 +463,6 @@ def main():
                            else f" (BASELINE configs[{k}] per GPU)")
     if rank == 0:
         cpu = cpu_baseline(args, scene) if world == 1 else None
-        import zlib
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -462,7 +490,7 @@ def main():
                 "bvh_nodes": st["bvhNodes"], "bvh_depth": st["bvhDepth"], "bvh_width": bvh_width,
                 "wave_threshold": pt._lib.hipptGetOption(hippt.OPT_WAVE_THRESHOLD),
                 "chunk": pt._lib.hipptGetOption(hippt.OPT_CHUNK),
-                "image_crc32": zlib.crc32(full.tobytes()) & 0xFFFFFFFF,
+                "image_crc32": image_crc,
                 **({"options": options} if options else {}),
             },
             "roofline": roofline,

@@ -68,3 +68,22 @@ def test_missing_reference_harness_is_reported_not_substituted(bench, monkeypatc
     a = _args(bench, [])
     cb = bench.cpu_baseline(a, types.SimpleNamespace(name="cornell34"))
     assert cb["value"] is None and cb["kind"] == "reference" and "missing" in cb["error"]
+
+
+def test_pmc_summary_used_only_for_the_same_run(bench):
+    """roofline.traffic comes from a PMC summary only when it describes this run —
+    the same image CRC and a rocprof kernel time within PMC_TIME_TOLERANCE of the live mean launch;
+    otherwise null, with the reason in roofline.pmc_refused."""
+    good = {"source": "profiles/x_pmc.json", "image_crc32": 2540294198, "mean_launch_ms_rocprof": 7.30,
+            "hbm_bytes_per_launch": 123}
+    pmc, why = bench.check_pmc(dict(good), 2540294198, 7.27, 1)
+    assert pmc and why is None
+    pmc, why = bench.check_pmc(dict(good, image_crc32=None), 2540294198, 7.27, 1)
+    assert pmc is None and "image_crc32" in why
+    pmc, why = bench.check_pmc(dict(good), 1209999578, 7.27, 1)
+    assert pmc is None and "CRC" in why
+    pmc, why = bench.check_pmc(dict(good, mean_launch_ms_rocprof=8.2), 2540294198, 7.27, 1)
+    assert pmc is None and "within" in why
+    pmc, why = bench.check_pmc(dict(good), 2540294198, 7.27, 8)
+    assert pmc is None and why
+    assert bench.check_pmc(None, 1, 1.0, 1) == (None, None)

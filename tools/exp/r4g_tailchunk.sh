@@ -19,3 +19,4 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT" || exit 1
 for k in 0 6; do
   timeout -k 10 200 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/r4g/prof_wf$k -o wf -- python3 -u bench.py --preset config5 --steps 2 --warmup 1 --cpu-baseline off --option WAVEFRONT_SORT=$k > gpurun_out/r4g/prof_wf$k.log 2>&1 || exit 1
 done
+timeout -k 10 1000 bash tools/profile.sh r4g_cornell > gpurun_out/r4g/profile.log 2>&1 || exit 1

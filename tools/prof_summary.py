@@ -107,6 +107,12 @@ def main():
         "ta_cycles_per_vmem_wave": round(c["TA_BUSY_avr"] * cus / c["TA_FLAT_READ_WAVEFRONTS_sum"], 2)
         if c.get("TA_BUSY_avr") and c.get("TA_FLAT_READ_WAVEFRONTS_sum") else None,
         "bench_value_msamples_s": bench["value"],
+        "bench_ms_per_step": bench["ms_per_step"],
+        # the profiled run's image: bench.py uses these counters only for a run of the same image
+        "image_crc32": cfg.get("image_crc32"),
+        # the kernel-trace run's own step time: the rocprof mean may not exceed it (same tree,
+        # same speed)
+        "rocprof_mean_le_ms_per_step": bool(mean_ms <= bench["ms_per_step"] * lps * 1.0005),
     }
     prof_dir = os.path.join(repo, a.out)
     name = a.name or tag
