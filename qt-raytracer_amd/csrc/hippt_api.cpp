@@ -549,9 +549,15 @@ bool ensure_order(Ctx &c, const CameraF &cam, int frames, int maxDepth, bool for
                 CostJob *j = job.get();
                 const int nt = std::max(1, cost_threads() / 2);
                 job->th = std::thread([j, nt] {
-                    hippt::run_costs(j->bvh, reinterpret_cast<const float *>(j->tris.data()), j->key.cam,
-                                     j->key.width, j->key.height, j->key.y0, j->key.rows, j->key.stride,
-                                     j->key.maxDepth, j->cost, nt);
+                    // an exception must not leave the thread (std::terminate): no estimate then,
+                    // and this key's batches stay in image order
+                    try {
+                        hippt::run_costs(j->bvh, reinterpret_cast<const float *>(j->tris.data()), j->key.cam,
+                                         j->key.width, j->key.height, j->key.y0, j->key.rows, j->key.stride,
+                                         j->key.maxDepth, j->cost, nt);
+                    } catch (...) {
+                        j->cost.clear();
+                    }
                     j->done.store(true, std::memory_order_release);
                 });
                 c.costJob = std::move(job);
@@ -564,6 +570,7 @@ bool ensure_order(Ctx &c, const CameraF &cam, int frames, int maxDepth, bool for
         c.orderKey = key;
         c.runCostsValid = true;
     }
+    if (c.runCosts.empty()) return true;  // no estimate for this key (its job failed): image order
     for (size_t k = 0; k < c.orderTables.size(); ++k)
         if (c.orderTables[k].frames == frames) {
             std::rotate(c.orderTables.begin(), c.orderTables.begin() + k, c.orderTables.begin() + k + 1);

@@ -167,7 +167,12 @@ void run_costs(const Bvh4 &bvh, const float *tris, const CameraF &cam, int width
     }
     std::vector<std::thread> pool;
     pool.reserve(nt - 1);
-    for (size_t k = 1; k < nt; ++k) pool.emplace_back(span, runs * k / nt, runs * (k + 1) / nt);
+    size_t k = 1;
+    try {
+        for (; k < nt; ++k) pool.emplace_back(span, runs * k / nt, runs * (k + 1) / nt);
+    } catch (...) {  // no more threads: the rest here (joinable threads must not be destroyed)
+        for (; k < nt; ++k) span(runs * k / nt, runs * (k + 1) / nt);
+    }
     span(0, runs / nt);
     for (auto &t : pool) t.join();
 }
