@@ -18,7 +18,6 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
-#include <cstdlib>
 #include <exception>
 #include <memory>
 #include <mutex>
@@ -60,15 +59,7 @@ constexpr int kTopOrderNodes = 1365;  // 6 complete levels
 // hippt_trace.h kQueues x kQueueStride work counters, then (its own line) the fused combine's
 // chunk counter (MeshParams::combCtr)
 constexpr size_t kCombCtrWord = 8 * 32;
-#ifdef HIPPT_PIPE_EXPERIMENT
-// then an overlapped batch's drain counters (MeshParams::drainCtr)
-constexpr size_t kDrainCtrWord = kCombCtrWord + 32;
-constexpr size_t kQueueBytes = (kCombCtrWord + 64) * sizeof(unsigned);
-constexpr int kPipeSlots = 2;
-constexpr size_t kPipeFlagStride = 32;
-#else
 constexpr size_t kQueueBytes = (kCombCtrWord + 32) * sizeof(unsigned);
-#endif
 
 struct EventPair {
     hipEvent_t a = nullptr, b = nullptr;
@@ -153,21 +144,6 @@ struct Ctx {
     std::shared_ptr<CostJob> costJob;  // automatic mode: the costs of a new key, off the render path
     int *spill = nullptr;      // 4-wide traversal: per-lane stack spill area
     size_t spillBytes = 0;
-#ifdef HIPPT_PIPE_EXPERIMENT
-    // overlapped batches (experiment build): per slot a stream, scratch, counters, spill area
-    struct PipeSlot {
-        hipStream_t stream = nullptr;
-        float *scratch = nullptr;
-        size_t scratchBytes = 0;
-        unsigned *queue = nullptr;
-        int *spill = nullptr;
-        size_t spillBytes = 0;
-    };
-    PipeSlot pipe[kPipeSlots];
-    unsigned *pipeFlags = nullptr;
-    unsigned pipeTicket = 0;
-    int pipePrev = -1, pipeNext = 0;
-#endif
     // wavefront path-state pool (allocated on first use)
     void *wfPool = nullptr;
     unsigned wfSlots = 0;  // slots allocated
@@ -941,70 +917,6 @@ bool copy_rows_async(Ctx &c, void *dstFrame, const void *src, size_t bytes, cons
     return true;
 }
 
-#ifdef HIPPT_PIPE_EXPERIMENT
-// Overlapped batches, measurement only (HIPPT_PIPE_EXPERIMENT builds, HIPPT_PIPE=1 in the
-// environment): batch j in slot j % 2 on the slot's stream, released by batch j-1's drain flag,
-// and NO combine (the images are not kept): the tails' overlap alone, timed.
-bool launch_overlapped(Ctx &c, hippt::MeshParams &p, long long blocks, bool spills, int spillCap, size_t scratchNeed,
-                       const char **err) {
-    const int k = c.pipeNext;
-    Ctx::PipeSlot &sl = c.pipe[k];
-    if (!c.pipeFlags) {
-        HIP_TRY(hipMalloc(&c.pipeFlags, kPipeSlots * kPipeFlagStride * sizeof(unsigned)));
-        HIP_TRY(hipMemset(c.pipeFlags, 0, kPipeSlots * kPipeFlagStride * sizeof(unsigned)));
-    }
-    if (!sl.stream) {
-        HIP_TRY(hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking));
-        HIP_TRY(hipMalloc(&sl.queue, kQueueBytes));
-    }
-    if (sl.scratchBytes < scratchNeed) {
-        HIP_TRY(hipDeviceSynchronize());
-        (void)hipFree(sl.scratch);
-        HIP_TRY(hipMalloc(&sl.scratch, scratchNeed));
-        sl.scratchBytes = scratchNeed;
-    }
-    if (spills) {
-        p.spillCap = spillCap;
-        const size_t bytes = size_t(blocks) * hippt::kMeshBlock * size_t(spillCap) * sizeof(int);
-        if (sl.spillBytes < bytes) {
-            HIP_TRY(hipDeviceSynchronize());
-            (void)hipFree(sl.spill);
-            HIP_TRY(hipMalloc(&sl.spill, bytes));
-            sl.spillBytes = bytes;
-        }
-        p.spill = sl.spill;
-    }
-    p.scratch = sl.scratch;
-    p.queue = sl.queue;
-    p.combCtr = sl.queue + kCombCtrWord;
-    p.drainCtr = sl.queue + kDrainCtrWord;
-    p.comb = hippt::CombineParams{};
-    HIP_TRY(hipMemsetAsync(sl.queue, 0, kQueueBytes, sl.stream));
-    if (c.pipePrev >= 0)
-        HIP_TRY(hipStreamWaitValue32(sl.stream, c.pipeFlags + size_t(c.pipePrev) * kPipeFlagStride, c.pipeTicket,
-                                     hipStreamWaitValueGte, 0xffffffffu));
-    p.drainFlag = c.pipeFlags + size_t(k) * kPipeFlagStride;
-    p.drainTicket = c.pipeTicket + 1;
-    EventPair ev;
-    if (!next_events(c, ev, err)) return false;
-    HIP_TRY(hipEventRecord(ev.a, sl.stream));
-    HIP_TRY(hippt::launch_mesh(p, int(blocks), false, sl.stream));
-    HIP_TRY(hipEventRecord(ev.b, sl.stream));
-    c.pending.push_back({0, ev});
-    HIP_TRY(hipStreamWriteValue32(sl.stream, p.drainFlag, p.drainTicket, 0));  // the backstop
-    c.pipeTicket = p.drainTicket;
-    c.pipePrev = k;
-    c.pipeNext = (k + 1) % kPipeSlots;
-    // the context's stream (sync points) waits for this batch
-    hipEvent_t e = nullptr;
-    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(e, sl.stream));
-    HIP_TRY(hipStreamWaitEvent(c.stream, e, 0));
-    (void)hipEventDestroy(e);
-    return true;
-}
-#endif
-
 // The deferred combine of a context as a launch of its own (see Ctx::deferred).
 bool flush_deferred(Ctx &c, const char **err) {
     if (!c.hasDeferred) return true;
@@ -1281,16 +1193,6 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                                                                       ldsScene ? numTris : 0, wide, topBytes,
                                                                       ldsScene ? numMats : 0));
                         if (s.rngTable && !rng_table(c, &p.rngTable, err)) return false;
-#ifdef HIPPT_PIPE_EXPERIMENT
-                        static const bool pipeEnv = std::getenv("HIPPT_PIPE") && std::atoi(std::getenv("HIPPT_PIPE")) > 0;
-                        if (pipeEnv && s.pathMode == 0 && !cnt && !copy) {
-                            long long blocks = (long long)c.cus * bpc;
-                            blocks = std::min<long long>(blocks, (total + hippt::kMeshBlock - 1) / hippt::kMeshBlock);
-                            blocks = std::max<long long>(blocks, 1);
-                            if (!launch_overlapped(c, p, blocks, spills, s.scene.stackBound4 + 3, need, err)) return false;
-                            continue;
-                        }
-#endif
                         if (s.pathMode == 1) {
                             if (!run_wavefront(c, p, cnt, spills, s.scene.stackBound4 + 3, err)) return false;
                         } else {

@@ -109,15 +109,7 @@ struct MeshParams {
     // claimed from *combCtr (zeroed with the work queue)
     CombineParams comb;
     unsigned *combCtr;
-    // Overlapped batches (experiment builds, -DHIPPT_PIPE_EXPERIMENT; DESIGN_LOG.md §A.0): the
-    // kernel raises *drainFlag to drainTicket once every block has started and a wave has found the
-    // queues drained (drainCtr[0]: block starts + kDrainBit, drainCtr[1]: the first drain's latch);
-    // the next batch's launch waits on it (hipStreamWaitValue32).  Null: not overlapped.
-    unsigned *drainFlag;
-    unsigned *drainCtr;
-    unsigned drainTicket;
 };
-constexpr unsigned kDrainBit = 1u << 24;
 
 
 // MeshParams::wide

@@ -286,17 +286,6 @@ __device__ __forceinline__ void pool_take(const MeshParams &P, const float *pool
     }
 }
 
-#ifdef HIPPT_PIPE_EXPERIMENT
-// Overlapped batches (MeshParams::drainFlag): the word the next batch's launch waits on, raised by
-// a vector atomic at system scope (the command processor polls it), once drainCtr[0] = blocks +
-// kDrainBit: every block has started (no block of this grid waits behind the next one) and a wave
-// has found the queues drained.
-__device__ __forceinline__ void drain_count(const MeshParams &P, unsigned add) {
-    if (atomicAdd(P.drainCtr, add) + add == gridDim.x + kDrainBit)
-        __hip_atomic_fetch_max(P.drainFlag, P.drainTicket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-#endif
-
 template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE, bool QUANT, bool SPILL = true, bool POOL = false,
           bool HYBRID = false, bool HALF = false>
 __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_EU : HIPPT_MESH_WAVES_PER_EU) HIPPT_SGPR_ATTR void mesh_kernel(MeshParams P) {
@@ -430,10 +419,6 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     };
 #endif
     unsigned waveThr = unsigned(P.waveThreshold);
-#ifdef HIPPT_PIPE_EXPERIMENT
-    if (P.drainFlag && threadIdx.x == 0) drain_count(P, 1u);
-    bool drainNoted = false;
-#endif
     bool combLeft = P.comb.bandPixels != 0;
     if (combLeft && (blockIdx.x & 1u) == 0 && threadIdx.x < 64u)
         while (combLeft) combLeft = combine_chunk(P);
@@ -500,24 +485,12 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                     fresh = true;
                 }
                 if (FINISH && __ballot(took && item == kNone)) waveThr = 0u;
-#ifdef HIPPT_PIPE_EXPERIMENT
-                if (P.drainFlag && !drainNoted && __ballot(took && item == kNone)) {
-                    drainNoted = true;
-                    if (__lane_id() == 0 && atomicCAS(P.drainCtr + 1, 0u, 1u) == 0u) drain_count(P, kDrainBit);
-                }
-#endif
             }
         } else if (__ballot(need)) {
             const unsigned it = order_item(P, queue_fetch(need, Q, P.queue, P.totalItems, P.chunk));
 #ifdef HIPPT_DEBUG_TIMELINE
             if (!tlDrained && __ballot(need && it == kNone)) tlDrained = __builtin_amdgcn_s_memrealtime();
             tlItems += __popcll(__ballot(it != kNone));
-#endif
-#ifdef HIPPT_PIPE_EXPERIMENT
-            if (P.drainFlag && !drainNoted && __ballot(need && it == kNone)) {
-                drainNoted = true;
-                if (__lane_id() == 0 && atomicCAS(P.drainCtr + 1, 0u, 1u) == 0u) drain_count(P, kDrainBit);
-            }
 #endif
             if (need) {
                 need = false;
