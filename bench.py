@@ -221,16 +221,18 @@ def cpu_baseline(args, scene) -> dict | None:
             "runs": [round(v, 4) for v in vals], "threads_rule": rule, "host": facts}
 
 
-def load_pmc(args, workload: str):
-    """HBM bytes per launch from a tools/profile.sh summary of this exact workload: --pmc, else
-    profiles/pmc_summary.json (the default workload), else the newest profiles/**/<name>_pmc.json."""
+def load_pmc(args, workload: str) -> list:
+    """The PMC summaries of this exact workload (tools/profile.sh + tools/prof_summary.py), most
+    recent first: --pmc, else profiles/pmc_summary.json (the default workload), then this round's
+    and older rounds' profiles/**/<name>_pmc.json, the archive last.  check_pmc picks the first that
+    describes this run."""
     prof = os.path.join(REPO, "profiles")
-    # this round's summaries first, then the rest (newest round first; the archive last)
     paths = [args.pmc] if args.pmc else (
         [os.path.join(prof, "pmc_summary.json")]
         + sorted(glob.glob(os.path.join(prof, "round*", "*_pmc.json")), reverse=True)
         + sorted(glob.glob(os.path.join(prof, "*_pmc.json")), reverse=True)
         + sorted(glob.glob(os.path.join(prof, "archive", "*_pmc.json")), reverse=True))
+    found = []
     for path in paths:
         try:
             with open(path) as f:
@@ -239,8 +241,8 @@ def load_pmc(args, workload: str):
             continue
         if d.get("workload") == workload:
             d["source"] = os.path.relpath(path, REPO)
-            return d
-    return None
+            found.append(d)
+    return found
 
 
 # PMC summaries older than this live run, or of another image, are not this run's traffic
@@ -248,9 +250,18 @@ PMC_TIME_TOLERANCE = 0.10
 
 
 def check_pmc(pmc, image_crc, mean_launch_ms: float, world: int):
-    """The PMC summary of this workload only where it describes this run: the same
+    """A PMC summary of this workload only where it describes this run: the same
     image (the summary's image_crc32 = this run's) and a kernel time within PMC_TIME_TOLERANCE of
-    this run's mean launch.  Otherwise (None, reason): roofline.traffic is null and says why."""
+    this run's mean launch.  `pmc`: one summary or load_pmc's list (the first that passes).
+    Otherwise (None, reason): roofline.traffic is null and says why (the first candidate's reason)."""
+    if isinstance(pmc, list):
+        first = None
+        for d in pmc:
+            ok, why = check_pmc(d, image_crc, mean_launch_ms, world)
+            if ok:
+                return ok, None
+            first = first or why
+        return None, first
     if not pmc:
         return None, None
     if world > 1:

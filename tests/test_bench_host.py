@@ -87,3 +87,16 @@ def test_pmc_summary_used_only_for_the_same_run(bench):
     pmc, why = bench.check_pmc(dict(good), 2540294198, 7.27, 8)
     assert pmc is None and why
     assert bench.check_pmc(None, 1, 1.0, 1) == (None, None)
+
+
+def test_pmc_candidates_first_consistent_wins(bench):
+    """load_pmc returns every summary of the workload; the first consistent one is used, an older
+    summary without a CRC does not hide a newer valid one."""
+    old = {"source": "profiles/round3/x_pmc.json", "image_crc32": None, "mean_launch_ms_rocprof": 18.9}
+    new = {"source": "profiles/round4/y_pmc.json", "image_crc32": 1209999578, "mean_launch_ms_rocprof": 18.88,
+           "hbm_bytes_per_launch": 7}
+    pmc, why = bench.check_pmc([old, new], 1209999578, 18.89, 1)
+    assert pmc is new and why is None
+    pmc, why = bench.check_pmc([old], 1209999578, 18.89, 1)
+    assert pmc is None and "image_crc32" in why
+    assert bench.check_pmc([], 1, 1.0, 1) == (None, None)
