@@ -124,7 +124,6 @@ struct Ctx {
     float4 *nodes4q = nullptr; // the 4-wide BVH with 8-bit child boxes
     float4 *nodes4h = nullptr; // hybrid layout (float top + 8-bit nodes) for hybridTop top nodes
     float4 *nodes4f = nullptr; // the 4-wide BVH with half-precision planes (half_bvh4; on use)
-    float4 *nodes4p = nullptr; // kPackedGlobal: index codes for packed keys (SceneHost::nodes4p)
     int halfVersion = -1;      // scene version of nodes4f
     int hybridTop = -1;
     // the queues' pixel-run order of this context's rows (HIPPT_OPT_ITEM_ORDER): run costs per key,
@@ -171,8 +170,6 @@ struct SceneHost {
     std::vector<float4> nodes4;                 // 4-wide BVH (bvh_builder.h Bvh4)
     std::vector<float4> nodes4q;                // quantize_bvh4 of it
     std::vector<float4> nodes4f;                // half_bvh4 of it (device codes; built on use)
-    std::vector<float4> nodes4p;                // kPackedGlobal: index codes masked to refBits4p (or empty)
-    unsigned refBits4p = 0;
     int halfState = 0;                          // nodes4f: 0 not built, 1 built, -1 out of half range
     hippt::Bvh4 bvh4;                           // the 4-wide tree with node-index codes ...
     std::vector<uint32_t> q4;                   // ... and its 8-bit nodes (hybrid_bvh4 inputs)
@@ -373,8 +370,7 @@ void free_scene_buffers(Ctx &c) {
     (void)hipFree(c.nodes4q);
     (void)hipFree(c.nodes4h);
     (void)hipFree(c.nodes4f);
-    (void)hipFree(c.nodes4p);
-    c.nodes = c.tris = c.shade = c.mats = c.nodes4 = c.nodes4q = c.nodes4h = c.nodes4f = c.nodes4p = nullptr;
+    c.nodes = c.tris = c.shade = c.mats = c.nodes4 = c.nodes4q = c.nodes4h = c.nodes4f = nullptr;
     c.halfVersion = -1;
     c.hybridTop = -1;
     drop_order(c);
@@ -486,8 +482,7 @@ bool ensure_scene(Ctx &c, const char **err) {
         return true;
     };
     if (!up(c.nodes, s.scene.nodes) || !up(c.tris, s.scene.tris) || !up(c.shade, s.scene.shade) ||
-        !up(c.mats, s.scene.mats) || !up(c.nodes4, s.scene.nodes4) || !up(c.nodes4q, s.scene.nodes4q) ||
-        !up(c.nodes4p, s.scene.nodes4p))
+        !up(c.mats, s.scene.mats) || !up(c.nodes4, s.scene.nodes4) || !up(c.nodes4q, s.scene.nodes4q))
         return false;
     c.sceneVersion = s.scene.version;
     return true;
@@ -1123,13 +1118,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         HIP_TRY(hipMemsetAsync(scratch, 0, size_t(total) * 3 * sizeof(float), c.stream));
                     } else {
                         hippt::MeshParams p{};
-                        // packed keys over the global float tree (kPackedGlobal builds: the megakernel)
-                        const bool packedG = hippt::kPackedGlobal && wide && !ldsScene && !quant && !half && !hybrid &&
-                                             s.pathMode == 0;
-                        if (packedG && s.scene.nodes4p.empty())
-                            return fail(err, "HIP path tracer: this build needs leaves of at most 4 primitives");
-                        p.nodes = hybrid ? c.nodes4h : quant ? c.nodes4q : half ? c.nodes4f : packedG ? c.nodes4p
-                                : wide ? c.nodes4 : c.nodes;
+                        p.nodes = hybrid ? c.nodes4h : quant ? c.nodes4q : half ? c.nodes4f : wide ? c.nodes4 : c.nodes;
                         p.tris = c.tris;
                         p.shade = c.shade;
                         p.mats = c.mats;
@@ -1186,7 +1175,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         p.wide = fmt;
                         p.stackCap = stackCap;
                         p.topBytes = topBytes;
-                        p.refBits = ldsScene && wide ? packed_ref_bits(numNodes, numTris) : packedG ? s.scene.refBits4p : 0u;
+                        p.refBits = ldsScene && wide ? packed_ref_bits(numNodes, numTris) : 0u;
                         p.rngTable = nullptr;
                         p.poolWords = poolWords;
                         // Pixel runs by estimated sample length, longest first, per XCD queue
@@ -1446,40 +1435,6 @@ extern "C" bool hipptUploadScene(const float *verts, const int *triMaterial, int
                 if (c >= 0) c *= stride;
             }
     };
-    // packed child keys over the tree in global memory (kPackedGlobal experiment builds): interior
-    // codes are node indices, leaf codes ~(first << 2 | (count - 1)), all masked to the low
-    // refBits4p bits (sign-extended in the kernel); none where a leaf holds more than 4 primitives
-    sc.nodes4p.clear();
-    sc.refBits4p = 0;
-    if (hippt::kPackedGlobal) {
-        std::vector<int32_t> w(reinterpret_cast<const int32_t *>(sc.nodes4.data()),
-                               reinterpret_cast<const int32_t *>(sc.nodes4.data()) + sc.nodes4.size() * 4);
-        const size_t n = w.size() / size_t(hippt::kNode4Words);
-        long long maxMag = (long long)n;
-        bool ok = true;
-        for (size_t k = 0; k < n && ok; ++k)
-            for (int i = 0; i < 4; ++i) {
-                int32_t &c = w[k * size_t(hippt::kNode4Words) + size_t(24 + i)];
-                if (c >= 0) continue;  // interior: its node index already
-                const int32_t code = ~c, first = code >> 4, count = code & 15;
-                if (count < 1 || count > 4) {
-                    ok = false;
-                    break;
-                }
-                c = ~(first << 2 | (count - 1));
-                maxMag = std::max(maxMag, (long long)(first << 2 | (count - 1)) + 1);
-            }
-        unsigned bits = 1;
-        while ((1ll << (bits - 1)) < maxMag) ++bits;
-        if (ok && bits <= 24) {
-            const uint32_t mask = (1u << bits) - 1u;
-            for (size_t k = 0; k < n; ++k)
-                for (int i = 0; i < 4; ++i) w[k * size_t(hippt::kNode4Words) + size_t(24 + i)] &= int32_t(mask);
-            sc.nodes4p.assign(sc.nodes4.size(), float4{});
-            std::memcpy(sc.nodes4p.data(), w.data(), w.size() * sizeof(int32_t));
-            sc.refBits4p = bits;
-        }
-    }
     byte_codes(sc.nodes4, hippt::kNode4Words, 24, hippt::kNode4Words * 4);
     byte_codes(sc.nodes4q, hippt::kNode4QWords, 12, hippt::kNode4QWords * 4);
     sc.nodes4f.clear();

@@ -112,13 +112,6 @@ struct MeshParams {
 };
 
 
-// Packed child keys over 4-wide float trees in global memory (experiment build flag; DESIGN_LOG.md
-// §A.0): the megakernel then reads MeshParams::nodes with index codes masked to refBits.
-#ifndef HIPPT_PACKED_GLOBAL
-#define HIPPT_PACKED_GLOBAL 0
-#endif
-constexpr bool kPackedGlobal = HIPPT_PACKED_GLOBAL != 0;
-
 // MeshParams::wide
 enum { kWide2 = 0, kWideFloat = 1, kWideQuant = 2, kWideHybrid = 3, kWideHalf = 4 };
 

@@ -313,8 +313,6 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     // 4.3% with them under the round-2 loop exits and gains 0.6% under the current ones,
     // cornell_mixed, round 3 A/Bs)
     constexpr bool PACKED = WIDE && LDS_SCENE && bool(HIPPT_PACKED_KEYS);
-    // the same over float trees in global memory (index codes, the host's nodes4p)
-    constexpr bool PACKED_G = kPackedGlobal && WIDE && !LDS_SCENE && !QUANT && !HYBRID && !HALF;
     int *const stk = LDS_SCENE ? lds + P.numNodes * ldsNodeF4 * 4 : lds + (TOP ? (P.topBytes >> 2) : 0u);
     int *const my = stk + threadIdx.x;
 
@@ -519,7 +517,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         if (!CAP || __any(busy(T))) do {
             prof<STATS>(pc, 2);
             if (WIDE)
-                traverse_round_wide<nodeF4, STATS, FULL, QUANT, SPILL, LDS_SCENE, TOP, HYBRID, PACKED || PACKED_G, HALF>(
+                traverse_round_wide<nodeF4, STATS, FULL, QUANT, SPILL, LDS_SCENE, TOP, HYBRID, PACKED, HALF>(
                     T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit, S, P.topBytes, P.refBits);
             else
                 traverse_round<nodeF4, STATS, FULL>(T, r, my, nodes, tris, nvis, ntest, pc, P.leafExit, P.nodeExit);

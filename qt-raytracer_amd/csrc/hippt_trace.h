@@ -605,12 +605,11 @@ __device__ __forceinline__ void test_prim(Trav &T, const Ray &r, const float4 *t
 // One leaf-loop iteration for this lane: the primitives of leaf T.leaf, then the next leaf if it
 // is next in line on the stack.  (Measured and rejected: one primitive per lane per iteration,
 // so that lanes with short leaves move on: Cornell -9%, blob70k -5%.)
-template <bool STATS, bool FULL, typename Pop, bool PAIRS = false, bool IDX = false>
+template <bool STATS, bool FULL, typename Pop, bool PAIRS = false>
 __device__ __forceinline__ void leaf_step(Trav &T, const Ray &r, const float4 *tris, unsigned long long &ntest,
                                           unsigned *pc, Pop pop) {
     const int code = ~T.leaf;
-    // IDX (packed keys over a global tree, HIPPT_PACKED_GLOBAL): ~(first << 2 | (count - 1))
-    const int first = IDX ? code >> 2 : code >> 4, last = first + (IDX ? (code & 3) + 1 : (code & 15));
+    const int first = code >> 4, last = first + (code & 15);
     if (PAIRS) {
         // two primitives' loads in flight per iteration (trees in global memory: blob70k +3%;
         // no gain from LDS)
@@ -860,10 +859,7 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
                                                     unsigned nodeExit, const SpillArea &S,
                                                     unsigned topBytes = 0, unsigned refBits = 0) {
     static_assert(!HYBRID || (QUANT && TOP), "hybrid trees: 8-bit nodes below an LDS top");
-    static_assert(!PACKED || !QUANT, "packed keys: float trees");
-    // packed keys over a tree in global memory (HIPPT_PACKED_GLOBAL): interior codes are node
-    // INDICES (byte offset = index << 7), leaf codes ~(first << 2 | (count - 1))
-    constexpr bool IDX = PACKED && !LDS0;
+    static_assert(!PACKED || (LDS0 && !QUANT), "packed keys: LDS-resident float trees");
     static_assert(!HALF || (TOP && !QUANT && !LDS0), "half planes: 4-wide trees in global memory");
     const unsigned refMask = PACKED ? (1u << refBits) - 1u : 0u;
     const float tmin = 0.001f;
@@ -874,10 +870,7 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
         // rows lo.x hi.x lo.y hi.y lo.z hi.z: read as near/far rows of this ray's octant (32-bit
         // byte offsets from the uniform base: base-register + offset-register loads).  NODE_F4
         // (the node stride) is implied by the codes: the device trees store byte offsets.
-        // node byte offset (IDX: index << 7 through an opaque shift, so that the compiler keeps the
-        // row addresses as nb | s, one v_or each, instead of splitting them into offsets)
-        unsigned nb = unsigned(T.cur);
-        if (IDX) asm volatile("v_lshlrev_b32 %0, 7, %1" : "=v"(nb) : "v"(T.cur));
+        const unsigned nb = unsigned(T.cur);  // interior codes are node byte offsets
         const bool topVisit = TOP && nb < topBytes;
         unsigned k0, k1, k2, k3;
         int4 ch;
@@ -1014,7 +1007,7 @@ __device__ __forceinline__ void traverse_round_wide(Trav &T, const Ray &r, int *
     auto popw = [&] { return pop_wide<SPILL, PACKED>(T, my, S, refBits); };
     while (T.leaf != 0) {
         prof<STATS>(pc, 4);
-        leaf_step<STATS, FULL, decltype(popw), !LDS0, IDX>(T, r, tris, ntest, pc, popw);
+        leaf_step<STATS, FULL, decltype(popw), !LDS0>(T, r, tris, ntest, pc, popw);
         if (nodeExit && __popcll(__ballot(T.leaf != 0)) <= nodeExit) break;
     }
 }
