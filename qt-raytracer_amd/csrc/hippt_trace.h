@@ -552,6 +552,21 @@ __device__ __forceinline__ void begin(Trav &T) {
     T.bestO = 0x7fffffff;
 }
 
+#ifndef HIPPT_FLAT_TRI
+#define HIPPT_FLAT_TRI 0
+#endif
+
+// A hit candidate (t >= tmin when `ok`) of primitive i (leaf order, original id `orig`) replaces the
+// closest hit when (t, orig) < (bestT, bestO).  Bitwise and selects: no branch per candidate (the
+// short-circuit form cost three exec-mask branches per triangle test).
+__device__ __forceinline__ void take_hit(Trav &T, float tt, bool ok, int i, int orig) {
+    const float tmin = 0.001f;
+    const bool win = ok & (tt >= tmin) & ((tt < T.bestT) | ((tt == T.bestT) & (orig < T.bestO)));
+    T.bestT = win ? tt : T.bestT;
+    T.bestI = win ? i : T.bestI;
+    T.bestO = win ? orig : T.bestO;
+}
+
 // Primitive i (leaf order) against the ray: closest hit = min (t, primitive id).
 template <bool STATS, bool FULL>
 __device__ __forceinline__ void test_prim_data(Trav &T, const Ray &r, float4 A, float4 B, float4 Cc, int i,
@@ -560,13 +575,9 @@ __device__ __forceinline__ void test_prim_data(Trav &T, const Ray &r, float4 A, 
     prof<STATS>(pc, 5);
     if (STATS) ++ntest;
     if (FULL && __float_as_int(Cc.z) != 0) {
-        float tt;
-        const int orig = __float_as_int(Cc.y);
-        if (sphere_t(A, B.x, r, tmin, tt) && (tt < T.bestT || (tt == T.bestT && orig < T.bestO))) {
-            T.bestT = tt;
-            T.bestI = i;
-            T.bestO = orig;
-        }
+        float tt = 0.0f;
+        const bool hit = sphere_t(A, B.x, r, tmin, tt);
+        take_hit(T, tt, hit, i, __float_as_int(Cc.y));
         return;
     }
     // Möller–Trumbore, division-free edge tests (pt_oracle.c po_tri_hit)
@@ -584,15 +595,13 @@ __device__ __forceinline__ void test_prim_data(Trav &T, const Ray &r, float4 A, 
     const float vn = fdot(r.dx, r.dy, r.dz, qvx, qvy, qvz);
     const bool neg = det < 0.0f;
     const float us = neg ? -un : un, vs = neg ? -vn : vn;
-    if (det != 0.0f && us >= 0.0f && vs >= 0.0f && us + vs <= fabsf(det)) {
-        const float tt = fdot(e2x, e2y, e2z, qvx, qvy, qvz) / det;
-        const int orig = __float_as_int(Cc.y);
-        if (tt >= tmin && (tt < T.bestT || (tt == T.bestT && orig < T.bestO))) {
-            T.bestT = tt;
-            T.bestI = i;
-            T.bestO = orig;
-        }
-    }
+    const bool inside = (det != 0.0f) & (us >= 0.0f) & (vs >= 0.0f) & (us + vs <= fabsf(det));
+#if HIPPT_FLAT_TRI
+    // the division for every lane, no branch at all
+    take_hit(T, fdot(e2x, e2y, e2z, qvx, qvy, qvz) / det, inside, i, __float_as_int(Cc.y));
+#else
+    if (inside) take_hit(T, fdot(e2x, e2y, e2z, qvx, qvy, qvz) / det, true, i, __float_as_int(Cc.y));
+#endif
 }
 
 template <bool STATS, bool FULL>
