@@ -552,10 +552,6 @@ __device__ __forceinline__ void begin(Trav &T) {
     T.bestO = 0x7fffffff;
 }
 
-#ifndef HIPPT_FLAT_TRI
-#define HIPPT_FLAT_TRI 0
-#endif
-
 // A hit candidate (t >= tmin when `ok`) of primitive i (leaf order, original id `orig`) replaces the
 // closest hit when (t, orig) < (bestT, bestO).  Bitwise and selects: no branch per candidate (the
 // short-circuit form cost three exec-mask branches per triangle test).
@@ -596,12 +592,8 @@ __device__ __forceinline__ void test_prim_data(Trav &T, const Ray &r, float4 A, 
     const bool neg = det < 0.0f;
     const float us = neg ? -un : un, vs = neg ? -vn : vn;
     const bool inside = (det != 0.0f) & (us >= 0.0f) & (vs >= 0.0f) & (us + vs <= fabsf(det));
-#if HIPPT_FLAT_TRI
-    // the division for every lane, no branch at all
-    take_hit(T, fdot(e2x, e2y, e2z, qvx, qvy, qvz) / det, inside, i, __float_as_int(Cc.y));
-#else
+    // (the division for every lane, without this branch: blob70k -1%, DESIGN_LOG.md §A.0)
     if (inside) take_hit(T, fdot(e2x, e2y, e2z, qvx, qvy, qvz) / det, true, i, __float_as_int(Cc.y));
-#endif
 }
 
 template <bool STATS, bool FULL>
