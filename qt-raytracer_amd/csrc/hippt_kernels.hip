@@ -216,6 +216,11 @@ __device__ unsigned long long g_rate[kRateSlots * kRateBuckets * 5];
 #define HIPPT_PACKED_KEYS 1
 #endif
 
+// Build knob (experiment): the camera sample's and item order's arguments loaded where a wave
+// generates camera rays instead of held in registers across the kernel (trace::late_arg_at).
+#ifndef HIPPT_LATE_CAM
+#define HIPPT_LATE_CAM 0
+#endif
 #ifndef HIPPT_WIDE_WAVES_PER_EU
 #define HIPPT_WIDE_WAVES_PER_EU 7
 #endif
@@ -449,7 +454,8 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                 }
                 if (n > avail) {
                     // the camera rays of the wave's next 64 items, every lane at once
-                    const unsigned it = order_item(P, queue_fetch(true, Q, P.queue, P.totalItems, P.chunk));
+                    const unsigned it = HIPPT_LATE_CAM ? order_item_late(queue_fetch(true, Q, P.queue, P.totalItems, P.chunk))
+                                                       : order_item(P, queue_fetch(true, Q, P.queue, P.totalItems, P.chunk));
 #ifdef HIPPT_DEBUG_TIMELINE
                     if (!tlDrained && __ballot(it == kNone)) tlDrained = __builtin_amdgcn_s_memrealtime();
                     tlItems += __popcll(__ballot(it != kNone));
@@ -458,7 +464,10 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                     uint32_t crng = 0;
                     if (it != kNone) {
                         prof<STATS>(pc, 1);
-                        camera_sample(P, it, c, crng);
+                        if (HIPPT_LATE_CAM)
+                            camera_sample(cam_args_late(), it, c, crng);
+                        else
+                            camera_sample(P, it, c, crng);
                     }
                     const unsigned k = __lane_id();
                     pool[k] = __uint_as_float(it);
@@ -487,7 +496,8 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                 if (FINISH && __ballot(took && item == kNone)) waveThr = 0u;
             }
         } else if (__ballot(need)) {
-            const unsigned it = order_item(P, queue_fetch(need, Q, P.queue, P.totalItems, P.chunk));
+            const unsigned it = HIPPT_LATE_CAM ? order_item_late(queue_fetch(need, Q, P.queue, P.totalItems, P.chunk))
+                                               : order_item(P, queue_fetch(need, Q, P.queue, P.totalItems, P.chunk));
 #ifdef HIPPT_DEBUG_TIMELINE
             if (!tlDrained && __ballot(need && it == kNone)) tlDrained = __builtin_amdgcn_s_memrealtime();
             tlItems += __popcll(__ballot(it != kNone));
@@ -497,7 +507,10 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                 item = it;
                 if (it != kNone) {
                     prof<STATS>(pc, 1);
-                    camera_sample(P, it, r, rng);
+                    if (HIPPT_LATE_CAM)
+                        camera_sample(cam_args_late(), it, r, rng);
+                    else
+                        camera_sample(P, it, r, rng);
                     tr = tg = tb = 1.0f;
                     depth = 0;
                     fresh = true;

@@ -262,6 +262,40 @@ __device__ __forceinline__ void prepare(Ray &r) {
     r.oiz = r.oz * r.iz;
 }
 
+// A MeshParams field (the kernels' only argument, at kernarg offset 0) loaded where it is used: the
+// opaque kernarg address keeps the compiler from loading it at kernel entry and holding it in
+// registers (SGPRs, or VGPR lanes once those run out) across the whole kernel.  Taking the
+// parameter's address instead would copy the whole block to scratch.
+template <typename T>
+__device__ __forceinline__ T late_arg_at(unsigned offset) {
+    typedef const char __attribute__((address_space(4))) *KPtr;
+    typedef const unsigned __attribute__((address_space(4))) *KWords;
+    static_assert(sizeof(T) % 4 == 0, "whole words");
+    KPtr k = (KPtr)__builtin_amdgcn_kernarg_segment_ptr();
+    asm volatile("" : "+s"(k));
+    const KWords w = reinterpret_cast<KWords>(k + offset);
+    T v;
+    unsigned *d = reinterpret_cast<unsigned *>(&v);
+#pragma unroll
+    for (unsigned i = 0; i < sizeof(T) / 4; ++i) d[i] = w[i];
+    return v;
+}
+
+// MeshParams from `cam` through `rcpWidth`: the camera sample's and the item order's arguments.
+// HIPPT_LATE_CAM builds load them where a wave generates camera rays (late_arg_at) instead of
+// holding ~30 uniform values across the kernel.
+struct CamArgs {
+    CameraF cam;
+    float invW, invH;
+    int width, height, y0, bandRows, rowStride;
+    int firstFrame, frames, maxDepth;
+    unsigned bandPixels, totalItems;
+    float rcpBandPixels, rcpWidth;
+};
+static_assert(offsetof(MeshParams, rcpWidth) - offsetof(MeshParams, cam) == offsetof(CamArgs, rcpWidth),
+              "CamArgs mirrors MeshParams");
+__device__ __forceinline__ CamArgs cam_args_late() { return late_arg_at<CamArgs>(unsigned(offsetof(MeshParams, cam))); }
+
 // Camera sample for work item `it`: RenderWorker::render u/v (RayTracerFboItem.cpp:109-110) and
 // Camera::get_ray (RayTracer.h:563-567, disk draw always consumed).
 // The work item at queue position `it` (MeshParams::runOrder, item_order.h build_item_table):
@@ -275,7 +309,22 @@ __device__ __forceinline__ unsigned order_item(const MeshParams &P, unsigned it)
     return run < P.runCount ? P.runOrder[fl * P.runCount + run] + (q & 63u) : it;
 }
 
-__device__ __forceinline__ void camera_sample(const MeshParams &P, unsigned it, Ray &r, uint32_t &rng) {
+// order_item with its arguments loaded where it runs (HIPPT_LATE_CAM)
+__device__ __forceinline__ unsigned order_item_late(unsigned it) {
+    if (it == kNone) return it;
+    const unsigned *order = late_arg_at<const unsigned *>(unsigned(offsetof(MeshParams, runOrder)));
+    if (!order) return it;
+    const CamArgs A = cam_args_late();
+    const unsigned runs = late_arg_at<unsigned>(unsigned(offsetof(MeshParams, runCount)));
+    unsigned fl, q;
+    divmod(it, A.bandPixels, A.rcpBandPixels, fl, q);
+    const unsigned run = q >> 6;
+    return run < runs ? order[fl * runs + run] + (q & 63u) : it;
+}
+
+// PP: MeshParams or CamArgs
+template <typename PP>
+__device__ __forceinline__ void camera_sample(const PP &P, unsigned it, Ray &r, uint32_t &rng) {
     unsigned fl, p, yb, x;
     divmod(it, P.bandPixels, P.rcpBandPixels, fl, p);
     divmod(p, unsigned(P.width), P.rcpWidth, yb, x);
