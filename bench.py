@@ -317,8 +317,36 @@ def make_roofline(args, pmc, traffic, mean_launch_ms, launches, alg_bytes_launch
     return r
 
 
+def free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launcher_command(argv: list, gpus: int, env) -> list | None:
+    """How `bench.py --gpus N` must run (never a silent one-GPU run).
+    None: this process is the run (N == 1, or a rank of a launcher whose WORLD_SIZE is N).  A list:
+    N > 1 without a launcher, so bench.py starts `torch.distributed.run` with N ranks on 127.0.0.1
+    as a child (before anything touches the GPU) and exits with its code.  A WORLD_SIZE that
+    disagrees with --gpus raises SystemExit (non-zero)."""
+    world = env.get("WORLD_SIZE")
+    if world is not None:
+        if int(world) != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but the launcher's WORLD_SIZE is {world}")
+        return None
+    if gpus <= 1:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__), *argv]
+
+
 def main():
     args = parse()
+    cmd = launcher_command(sys.argv[1:], args.gpus, os.environ)
+    if cmd is not None:
+        log("bench.py: --gpus", args.gpus, "without a launcher: starting", " ".join(cmd[1:6]), "...")
+        raise SystemExit(subprocess.run(cmd).returncode)
     import torch  # noqa: F401  (torch.distributed for the rank barrier / max-over-ranks)
     import torch.distributed as dist
     import hippt
@@ -337,8 +365,6 @@ def main():
             sys.stdout.flush()
             os.dup2(saved, 1)
             os.close(saved)
-    if world != args.gpus:
-        log(f"note: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE")
     lib = hippt.load_library()
     ndev = lib.hipptDeviceCount()
     if ndev < 1:
@@ -502,6 +528,12 @@ def main():
                 "wave_threshold": pt._lib.hipptGetOption(hippt.OPT_WAVE_THRESHOLD),
                 "chunk": pt._lib.hipptGetOption(hippt.OPT_CHUNK),
                 "image_crc32": image_crc,
+                # the library default is -1 (automatic: the estimate on a host thread, batches queued
+                # meanwhile in image order); bench.py forces it
+                "item_order": {"option": 1, "library_default": -1,
+                               "note": "run-cost estimate computed on the first (counted, untimed) call, "
+                                       "before the timed region: the timed steps are a fixed camera's "
+                                       "steady state"},
                 **({"options": options} if options else {}),
             },
             "roofline": roofline,

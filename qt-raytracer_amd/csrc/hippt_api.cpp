@@ -16,12 +16,14 @@
 #include <algorithm>
 #include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstring>
 #include <exception>
 #include <memory>
 #include <mutex>
 #include <string>
+#include <system_error>
 #include <thread>
 #include <utility>
 #include <vector>
@@ -88,15 +90,27 @@ bool same_key(const OrderKey &a, const OrderKey &b) {
     return true;
 }
 
-// Run costs computed on a host thread of their own (HIPPT_OPT_ITEM_ORDER automatic): the thread
-// reads only the job's copies of the tree and primitives, so scene uploads and renders go on.
+// Run costs computed on a detached host thread (HIPPT_OPT_ITEM_ORDER automatic).  The thread owns a
+// reference to its job and reads only the job's copies of the tree and primitives, so scene uploads,
+// renders and process exit never wait for it: a context that no longer wants the result drops its
+// reference (abandon_cost_job), and no joinable std::thread is ever destroyed (a
+// function-local static State destroyed at exit with a joinable thread called std::terminate).
 struct CostJob {
     OrderKey key;
     hippt::Bvh4 bvh;
     std::vector<float4> tris;
     std::vector<float> cost;
-    std::atomic<bool> done{false};
-    std::thread th;
+    std::mutex mu;
+    std::condition_variable cv;
+    bool done = false;
+    bool finished() {
+        std::lock_guard<std::mutex> g(mu);
+        return done;
+    }
+    void wait() {
+        std::unique_lock<std::mutex> g(mu);
+        cv.wait(g, [this] { return done; });
+    }
 };
 
 struct Ctx {
@@ -347,14 +361,12 @@ void retire_table(Ctx &c, unsigned *dev) {
     c.retiredTables.push_back({dev, e});
 }
 
-void join_cost_job(Ctx &c) {
-    if (c.costJob && c.costJob->th.joinable()) c.costJob->th.join();
-    c.costJob.reset();
-}
+// The context stops waiting for its cost job; the detached thread finishes on its own reference.
+void abandon_cost_job(Ctx &c) { c.costJob.reset(); }
 
 // Forgets the run costs and every item table (scene buffers freed, context destroyed).
 void drop_order(Ctx &c) {
-    join_cost_job(c);
+    abandon_cost_job(c);
     for (auto &t : c.orderTables) retire_table(c, t.dev);
     c.orderTables.clear();
     c.orderKey = OrderKey{};
@@ -531,36 +543,46 @@ bool ensure_order(Ctx &c, const CameraF &cam, int frames, int maxDepth, bool for
     free_retired_tables(c, false);
     if (!c.runCostsValid || !same_key(key, c.orderKey)) {
         std::vector<float> cost;
-        if (c.costJob && c.costJob->done.load(std::memory_order_acquire) && same_key(c.costJob->key, key)) {
-            c.costJob->th.join();
+        const bool jobForKey = c.costJob && same_key(c.costJob->key, key);
+        if (jobForKey && (forced || c.costJob->finished())) {
+            // forced mode takes the in-flight job's estimate for this key rather than computing it
+            // again
+            c.costJob->wait();
             cost = std::move(c.costJob->cost);
             c.costJob.reset();
         } else if (forced) {
-            join_cost_job(c);
+            abandon_cost_job(c);  // a stale key's job: not joined on the render path
             hippt::run_costs(s.scene.bvh4, reinterpret_cast<const float *>(s.scene.tris.data()), cam, s.width,
                              s.height, c.y0, c.rows, c.stride, maxDepth, cost, cost_threads());
         } else {
-            if (c.costJob && c.costJob->done.load(std::memory_order_acquire)) join_cost_job(c);  // a stale key
+            if (c.costJob && !jobForKey) abandon_cost_job(c);
             if (!c.costJob) {
                 auto job = std::make_shared<CostJob>();
                 job->key = key;
                 job->bvh = s.scene.bvh4;
                 job->tris = s.scene.tris;
-                CostJob *j = job.get();
                 const int nt = std::max(1, cost_threads() / 2);
-                job->th = std::thread([j, nt] {
-                    // an exception must not leave the thread (std::terminate): no estimate then,
-                    // and this key's batches stay in image order
-                    try {
-                        hippt::run_costs(j->bvh, reinterpret_cast<const float *>(j->tris.data()), j->key.cam,
-                                         j->key.width, j->key.height, j->key.y0, j->key.rows, j->key.stride,
-                                         j->key.maxDepth, j->cost, nt);
-                    } catch (...) {
-                        j->cost.clear();
-                    }
-                    j->done.store(true, std::memory_order_release);
-                });
-                c.costJob = std::move(job);
+                try {
+                    std::thread([job, nt] {
+                        // an exception must not leave the thread (std::terminate): no estimate then,
+                        // and this key's batches stay in image order
+                        try {
+                            hippt::run_costs(job->bvh, reinterpret_cast<const float *>(job->tris.data()),
+                                             job->key.cam, job->key.width, job->key.height, job->key.y0,
+                                             job->key.rows, job->key.stride, job->key.maxDepth, job->cost, nt);
+                        } catch (...) {
+                            job->cost.clear();
+                        }
+                        {
+                            std::lock_guard<std::mutex> g(job->mu);
+                            job->done = true;
+                        }
+                        job->cv.notify_all();
+                    }).detach();
+                    c.costJob = std::move(job);
+                } catch (const std::system_error &) {
+                    // no thread to be had: this batch in image order, the next one tries again
+                }
             }
             return true;  // this batch in image order
         }
@@ -1273,12 +1295,14 @@ extern "C" bool cudaPathTracerRender(int frameIndex, int maxDepth, const unsigne
     std::lock_guard<std::mutex> g(S().mu);
     // the CUDA backend's ABI always hands out its ARGB words (HIPPT_OPT_PIXEL_FORMAT applies to
     // the hippt* render calls)
-    State &s = S();
-    const int format = s.pixelFormat;
-    s.pixelFormat = HIPPT_PIXEL_ARGB;
-    const bool ok = render_locked(frameIndex, 1, maxDepth, hostPixels, errorMessage);
-    s.pixelFormat = format;
-    return ok;
+    // (restored on every way out, an exception caught below included: ADVICE r4)
+    struct FormatScope {
+        int &fmt;
+        const int saved;
+        ~FormatScope() { fmt = saved; }
+    } scope{S().pixelFormat, S().pixelFormat};
+    scope.fmt = HIPPT_PIXEL_ARGB;
+    return render_locked(frameIndex, 1, maxDepth, hostPixels, errorMessage);
 } catch (const std::exception &e) {
     return fail_free(errorMessage, e.what());
 } catch (...) {

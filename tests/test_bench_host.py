@@ -100,3 +100,22 @@ def test_pmc_candidates_first_consistent_wins(bench):
     pmc, why = bench.check_pmc([old], 1209999578, 18.89, 1)
     assert pmc is None and "image_crc32" in why
     assert bench.check_pmc([], 1, 1.0, 1) == (None, None)
+
+
+def test_gpus_without_launcher_starts_ranks_or_fails(bench):
+    """`bench.py --gpus N` never falls back silently to one GPU.  Without a launcher
+    (no WORLD_SIZE) N > 1 becomes a torch.distributed.run child with N ranks on 127.0.0.1 and the
+    same arguments; under a launcher WORLD_SIZE must equal --gpus, else a non-zero exit."""
+    assert bench.launcher_command(["--steps", "3"], 1, {}) is None
+    cmd = bench.launcher_command(["--gpus", "8", "--steps", "3"], 8, {})
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=8" in cmd and cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-4:] == [os.path.join(REPO, "bench.py"), "--gpus", "8", "--steps", "3"][-4:]
+    assert cmd[-5].endswith("bench.py")
+    assert bench.launcher_command(["--gpus", "4"], 4, {"WORLD_SIZE": "4"}) is None
+    assert bench.launcher_command([], 1, {"WORLD_SIZE": "1"}) is None
+    with pytest.raises(SystemExit) as e:
+        bench.launcher_command(["--gpus", "8"], 8, {"WORLD_SIZE": "2"})
+    assert e.value.code != 0
+    with pytest.raises(SystemExit):
+        bench.launcher_command([], 1, {"WORLD_SIZE": "4"})
