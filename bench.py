@@ -245,19 +245,26 @@ def load_pmc(args, workload: str) -> list:
     return found
 
 
-# PMC summaries older than this live run, or of another image, are not this run's traffic
-PMC_TIME_TOLERANCE = 0.10
+def lib_sha256(path: str) -> str | None:
+    import hashlib
+    try:
+        with open(path, "rb") as f:
+            return hashlib.sha256(f.read()).hexdigest()
+    except OSError:
+        return None
 
 
-def check_pmc(pmc, image_crc, mean_launch_ms: float, world: int):
-    """A PMC summary of this workload only where it describes this run: the same
-    image (the summary's image_crc32 = this run's) and a kernel time within PMC_TIME_TOLERANCE of
-    this run's mean launch.  `pmc`: one summary or load_pmc's list (the first that passes).
-    Otherwise (None, reason): roofline.traffic is null and says why (the first candidate's reason)."""
+def check_pmc(pmc, image_crc, lib_sha, world: int):
+    """A PMC summary of this workload only where it describes this run: the
+    same image (the summary's image_crc32 = this run's) traced by the same kernels (the summary's
+    lib_sha256 = the loaded libhippt.so's).  Its bytes are per step, so a profile taken on a slower
+    box still states this run's traffic; the line's HBM rate divides them by this run's kernel time.
+    `pmc`: one summary or load_pmc's list (the first that passes).  Otherwise (None, reason):
+    roofline.traffic is null and says why (the first candidate's reason)."""
     if isinstance(pmc, list):
         first = None
         for d in pmc:
-            ok, why = check_pmc(d, image_crc, mean_launch_ms, world)
+            ok, why = check_pmc(d, image_crc, lib_sha, world)
             if ok:
                 return ok, None
             first = first or why
@@ -270,33 +277,36 @@ def check_pmc(pmc, image_crc, mean_launch_ms: float, world: int):
         return None, f"{pmc.get('source')}: no image_crc32 recorded (profile predates the check)"
     if image_crc is not None and int(pmc["image_crc32"]) != int(image_crc):
         return None, f"{pmc.get('source')}: image CRC {pmc['image_crc32']} is not this run's {image_crc}"
-    prof_ms = pmc.get("mean_launch_ms_rocprof")
-    if not prof_ms or mean_launch_ms <= 0 or abs(prof_ms - mean_launch_ms) > PMC_TIME_TOLERANCE * mean_launch_ms:
-        return None, (f"{pmc.get('source')}: rocprof mean {prof_ms} ms is not within "
-                      f"{PMC_TIME_TOLERANCE:.0%} of this run's {mean_launch_ms:.4f} ms per launch")
+    if not pmc.get("lib_sha256") or pmc["lib_sha256"] != lib_sha:
+        return None, f"{pmc.get('source')}: profiled libhippt.so {str(pmc.get('lib_sha256'))[:12]} is not this run's {str(lib_sha)[:12]}"
+    if not pmc.get("hbm_bytes_per_step"):
+        return None, f"{pmc.get('source')}: no per-step byte count (profile predates round 5)"
     return pmc, None
 
 
-def make_roofline(args, pmc, traffic, mean_launch_ms, launches, alg_bytes_launch, flops_launch, counted,
-                  alg_gbs) -> dict:
+def make_roofline(args, pmc, traffic, kernel_ms_step, launches, alg_bytes_step, flops_step, counted,
+                  alg_gbs, mean_launch_ms) -> dict:
     """Roofline of the dominant kernel.  This path is branchy scalar FP32 over a cache-resident
     scene: neither HBM nor MFMA bounds it.  The headline roofline is the FP32 VALU one
-    (algorithmic FLOP per launch from the counted pass / live mean launch time, vs the FP32
-    vector peak); `limiter` names the busiest unit in this workload's PMC profile (VALU issue,
-    the vector-memory texture addresser TA, or HBM), and the HBM fraction is computed from the
-    PMC-measured DRAM bytes, not from the modelled node/primitive bytes (those are served by
-    LDS/L2/MALL; reported as algorithmic_bytes)."""
-    s = mean_launch_ms * 1e-3
-    tflops = flops_launch / s / 1e12 if s > 0 else 0.0
+    (algorithmic FLOP per step from the counted pass / the mesh kernel's live time per step, HIP
+    events on the library's stream, vs the FP32 vector peak).  Per step, not per launch: chained
+    batches (HIPPT_OPT_CHAIN) spread a run's steps over fewer tracing launches, so a launch's
+    duration is not a step's.  `limiter` names the busiest unit in this workload's PMC profile (VALU
+    issue, the vector-memory texture addresser TA, or HBM), and the HBM fraction is computed from the
+    PMC-measured DRAM bytes per step (calibrated, tools/micro/pmc_bytes.hip), not from the modelled
+    node/primitive bytes (those are served by LDS/L2/MALL; reported as algorithmic_bytes)."""
+    s = kernel_ms_step * 1e-3
+    tflops = flops_step / s / 1e12 if s > 0 else 0.0
     r = {"bound": "valu", "achieved": round(tflops, 3), "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
          "frac": round(tflops / FP32_PEAK_TFLOPS, 4), "traffic": traffic,
          "kernel": "mesh_kernel" if args.path_mode == "megakernel" else "wf_extend+wf_shade+wf_generate",
-         "mean_launch_ms": round(mean_launch_ms, 4), "launches_per_step": launches,
-         "flop_per_launch": int(flops_launch),
+         "kernel_ms_per_step": round(kernel_ms_step, 4), "launches_per_step": launches,
+         "mean_launch_ms": round(mean_launch_ms, 4),
+         "flop_per_step": int(flops_step),
          "model": "20 FLOP per child-box slab test (2 per 2-wide, 4 per 4-wide node visit), 55 per primitive "
                   "test, 100 per shading step",
          "node_visits_per_step": counted["nodeVisits"], "tri_tests_per_step": counted["triTests"],
-         "algorithmic_bytes": {"per_launch": int(alg_bytes_launch), "achieved_gbs": round(alg_gbs, 2),
+         "algorithmic_bytes": {"per_step": int(alg_bytes_step), "achieved_gbs": round(alg_gbs, 2),
                                "note": "node/primitive/shading bytes of the traversal (SURVEY.md 8d), served "
                                        "from LDS/L2/MALL; not HBM traffic"}}
     if pmc:
@@ -309,9 +319,10 @@ def make_roofline(args, pmc, traffic, mean_launch_ms, launches, alg_bytes_launch
         r["ta_busy"] = pmc.get("ta_busy")
         r["hbm"] = {"achieved": round(hbm, 2) if hbm is not None else None, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(hbm / HBM_PEAK_GBS, 4) if hbm is not None else None,
-                    "note": "PMC DRAM bytes per launch (FETCH_SIZE + WRITE_SIZE) / live mean launch time"}
+                    "note": "PMC DRAM bytes per step (FETCH_SIZE and WRITE_SIZE with the calibrated factors of "
+                            "traffic_model) / this run's kernel time per step"}
+        r["traffic_model"] = pmc.get("traffic_model")
         r["pmc_source"] = pmc.get("source")
-        r["mean_launch_ms_rocprof"] = pmc.get("mean_launch_ms_rocprof")
     else:
         r["limiter"] = None
     return r
@@ -465,17 +476,17 @@ def main():
     # PMC summary's check)
 
     # roofline of the dominant (mesh) kernel, from this rank's counted pass and live events
-    launches = max(1, st["traceLaunches"] // max(1, args.steps))
+    launches = round(st["traceLaunches"] / max(1, args.steps), 3)
     bytes_node = BYTES_NODE if bvh_width != 4 else BYTES_NODE4
     flop_node = FLOP_NODE if bvh_width != 4 else 2 * FLOP_NODE
     alg_bytes_step = (bytes_node * counted["nodeVisits"] + BYTES_TRI * counted["triTests"]
                       + BYTES_SHADE * (counted["segments"] - counted["pixelSamples"])
                       + BYTES_SAMPLE * counted["pixelSamples"])
-    alg_bytes_launch = alg_bytes_step / launches
-    flops_launch = (flop_node * counted["nodeVisits"] + FLOP_TRI * counted["triTests"]
-                    + FLOP_SHADE * counted["segments"]) / launches
+    flops_step = (flop_node * counted["nodeVisits"] + FLOP_TRI * counted["triTests"]
+                  + FLOP_SHADE * counted["segments"])
+    kernel_ms_step = st["traceMs"] / max(1, args.steps)
     mean_launch_ms = st["traceMs"] / max(1, st["traceLaunches"])
-    achieved = alg_bytes_launch / (mean_launch_ms * 1e-3) / 1e9 if mean_launch_ms > 0 else 0.0
+    achieved = alg_bytes_step / (kernel_ms_step * 1e-3) / 1e9 if kernel_ms_step > 0 else 0.0
     workload = f"{args.scene} {args.width}x{args.height} {frames}spp depth{args.depth}"
     if args.path_mode == "wavefront":
         workload += " wavefront"
@@ -485,11 +496,11 @@ def main():
             else hd.gather_bands(px, args.height, dist))
     import zlib
     image_crc = zlib.crc32(full.tobytes()) & 0xFFFFFFFF if full is not None else None
-    pmc, pmc_refused = check_pmc(pmc, image_crc, mean_launch_ms, world)
-    traffic = pmc.get("hbm_bytes_per_launch") if pmc else None
+    pmc, pmc_refused = check_pmc(pmc, image_crc, lib_sha256(os.environ.get("HIPPT_LIB") or hippt.LIB_PATH), world)
+    traffic = pmc.get("hbm_bytes_per_step") if pmc else None
 
-    roofline = make_roofline(args, pmc, traffic, mean_launch_ms, launches, alg_bytes_launch, flops_launch,
-                             counted, achieved)
+    roofline = make_roofline(args, pmc, traffic, kernel_ms_step, launches, alg_bytes_step, flops_step,
+                             counted, achieved, mean_launch_ms)
     if pmc_refused:
         roofline["pmc_refused"] = pmc_refused
 
@@ -530,6 +541,11 @@ def main():
                 "image_crc32": image_crc,
                 # the library default is -1 (automatic: the estimate on a host thread, batches queued
                 # meanwhile in image order); bench.py forces it
+                "chain": {"option": pt._lib.hipptGetOption(hippt.OPT_CHAIN),
+                          "note": "HIPPT_OPT_CHAIN (default -1, automatic): one launch is enqueued per step; "
+                                  "a launch whose batch is drained goes on with the steps posted behind it "
+                                  "(ring of batches, hippt_trace.h), the next launch combines them; every "
+                                  "step's frames are traced and combined inside the timed region"},
                 "item_order": {"option": 1, "library_default": -1,
                                "note": "run-cost estimate computed on the first (counted, untimed) call, "
                                        "before the timed region: the timed steps are a fixed camera's "

@@ -244,6 +244,15 @@ enum {
                                        direction octant (3) or octant and a 2x2x2 cell of the scene box (6),
                                        so that a wave of the extend kernel traces rays of one kind; 0: in
                                        thread order; -1 (default): automatic (0).  Same results either way */
+    , HIPPT_OPT_CHAIN = 30          /* megakernel, camera-pool kernels over 4-wide float nodes: asynchronous
+                                       batches with the same scene, camera, rows and frames per batch (each
+                                       the same frames again or the next ones) form a run, and a launch whose
+                                       batch is drained goes on with the batches posted behind it, up to this
+                                       many (1..8), so that the run pays the launch's tail once per that many
+                                       batches; the next launch combines them beside its own paths and the
+                                       image's readers flush the rest.  0: one launch per batch; -1
+                                       (default): automatic (on, 2..8 batches by the batch's size).  Same
+                                       results either way */
 };
 /* Output frame word formats (HIPPT_OPT_PIXEL_FORMAT).  Both map an accumulated colour c to
  * sqrt(clamp(c, 0, 1)) per channel.

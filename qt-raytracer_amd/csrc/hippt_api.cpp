@@ -170,6 +170,30 @@ struct Ctx {
     int cus = 0;
     long long occKey = -1;  // occupancy cached per (scene version, depth, lds, full)
     int meshBlocksPerCu[2] = {0, 0};
+    int meshBlocksPerCuChain = 0;  // the chained-batch kernel's
+    // Chained batches (HIPPT_OPT_CHAIN; MeshParams::chain*, hippt_trace.h): the open run.  Its launches
+    // share a ring of `slots` scratch slots and work-counter blocks (chainCtl, zeroed when a run
+    // starts); the host posts each batch in the mailbox (run << 33 | consecutive << 32 | batch) before
+    // its launch is enqueued, and the run's last combines are a flush before anything reads or
+    // resets the image (flush_deferred).
+    struct Chain {
+        bool live = false;   // a run is open
+        unsigned run = 0;    // its id
+        unsigned seq = 0;    // the next batch's number in the run
+        unsigned epoch = 0;  // the next launch's number in the run
+        int firstFrame = 0;  // batch 0's first frame
+        int step = -1;       // frames from one batch to the next (-1: one batch so far)
+        unsigned slots = 0, shift = 0, cap = 0;
+        hippt::MeshParams key{};  // what every batch of the run shares (chain_same)
+        long long blocks = 0;
+    } chain;
+    unsigned *chainCtl = nullptr;
+    float *chainScratch = nullptr;
+    size_t chainScratchBytes = 0;
+    unsigned long long *chainBox = nullptr;     // pinned, coherent mailbox word
+    unsigned long long *chainBoxDev = nullptr;  // its device address
+    // pixel samples of chained batches (their kernels do not count them: every item is one sample)
+    unsigned long long hostSamples = 0;
     std::vector<EventPair> pool;                         // every timing event pair created
     std::vector<EventPair> freeEv;                       // pairs not in flight
     std::vector<std::pair<int, EventPair>> pending;      // (0 trace / 1 combine, events)
@@ -235,6 +259,7 @@ struct State {
     int cameraPool = -1;  // megakernel camera-ray pool (HIPPT_OPT_CAMERA_POOL; -1: automatic)
     int fuseCombine = -1;  // combine inside the next megakernel launch (HIPPT_OPT_FUSE_COMBINE)
     int itemOrder = -1;    // scene-hitting pixel runs first (HIPPT_OPT_ITEM_ORDER; -1: automatic)
+    int chainBatches = -1; // batches a chained launch may trace (HIPPT_OPT_CHAIN; 0 off, -1 automatic)
     std::vector<std::pair<int, uint32_t *>> rngTables;  // per device, built on first use
     unsigned activeTopBytes = 0;  // of the last mesh render (hipptGetOption HIPPT_INFO_*)
     int activeBlocksPerCu = 0;
@@ -400,6 +425,9 @@ void destroy_ctx(Ctx &c) {
     c.scratchAltBytes = 0;
     c.hasDeferred = false;
     (void)hipFree(c.queue);
+    (void)hipFree(c.chainCtl);
+    (void)hipFree(c.chainScratch);
+    if (c.chainBox) (void)hipHostFree(c.chainBox);
     (void)hipFree(c.stats);
     (void)hipFree(c.wfPool);
     (void)hipFree(c.wfCtr);
@@ -939,8 +967,35 @@ bool copy_rows_async(Ctx &c, void *dstFrame, const void *src, size_t bytes, cons
     return true;
 }
 
-// The deferred combine of a context as a launch of its own (see Ctx::deferred).
+// The open chain run's last combines (Ctx::chain): every batch no launch combined, in order; the run
+// ends (the next chained batch starts a new one).
+bool flush_chain(Ctx &c, const char **err) {
+    Ctx::Chain &ch = c.chain;
+    if (!ch.live) return true;
+    ch.live = false;
+    HIP_TRY(hipSetDevice(c.device));
+    hippt::ChainFlushParams f{};
+    f.comb = ch.key.comb;
+    f.scratch = c.chainScratch;
+    f.ctl = c.chainCtl;
+    f.epoch = ch.epoch;  // the run's launches were epochs 0 .. epoch - 1
+    f.lastSeq = ch.seq - 1u;
+    f.slots = ch.slots;
+    f.shift = ch.shift;
+    f.step = std::max(ch.step, 0);
+    EventPair ev;
+    if (!next_events(c, ev, err)) return false;
+    HIP_TRY(hipEventRecord(ev.a, c.stream));
+    HIP_TRY(hippt::launch_chain_flush(f, c.stream));
+    HIP_TRY(hipEventRecord(ev.b, c.stream));
+    c.pending.push_back({1, ev});
+    return true;
+}
+
+// The deferred combine of a context as a launch of its own (see Ctx::deferred), or the open chain
+// run's flush.
 bool flush_deferred(Ctx &c, const char **err) {
+    if (!flush_chain(c, err)) return false;
     if (!c.hasDeferred) return true;
     c.hasDeferred = false;
     HIP_TRY(hipSetDevice(c.device));
@@ -968,6 +1023,123 @@ bool batch_scratch(Ctx &c, size_t need, float **out, const char **err) {
         bytes = need;
     }
     *out = buf;
+    return true;
+}
+
+// Chained batches (Ctx::chain).  Automatic: a launch traces up to ~4e8 samples' worth of batches (3 of
+// a whole 1080p/64 spp image, 8 of its 1/4 and 1/8 row shares); the ring holds twice that, so that a
+// launch traces one group of batches while it combines the previous one.
+// automatic (HIPPT_OPT_CHAIN -1): chained batches on or off
+constexpr bool kChainAuto = false;
+
+unsigned chain_cap(long long option, unsigned total) {
+    if (option > 0) return unsigned(std::min<long long>(option, 8));
+    const double c = std::round(4e8 / double(std::max(1u, total)));
+    return unsigned(std::clamp(c, 2.0, 8.0));
+}
+
+bool same_cam(const CameraF &a, const CameraF &b) {
+    if (a.lens_radius != b.lens_radius) return false;
+    for (int k = 0; k < 3; ++k)
+        if (a.origin[k] != b.origin[k] || a.llc[k] != b.llc[k] || a.horizontal[k] != b.horizontal[k] ||
+            a.vertical[k] != b.vertical[k] || a.u[k] != b.u[k] || a.v[k] != b.v[k])
+            return false;
+    return true;
+}
+
+// Two batches' launch parameters agree on everything the run's launches take from their own
+// parameters for every batch of the run (all but the frames, scratch, counters and chain fields).
+bool chain_same(const hippt::MeshParams &a, const hippt::MeshParams &b) {
+    return a.nodes == b.nodes && a.tris == b.tris && a.shade == b.shade && a.mats == b.mats && a.stats == b.stats &&
+           same_cam(a.cam, b.cam) && a.invW == b.invW && a.invH == b.invH && a.width == b.width &&
+           a.height == b.height && a.y0 == b.y0 && a.bandRows == b.bandRows && a.rowStride == b.rowStride &&
+           a.frames == b.frames && a.maxDepth == b.maxDepth && a.bandPixels == b.bandPixels &&
+           a.totalItems == b.totalItems && a.stackDepth == b.stackDepth && a.numNodes == b.numNodes &&
+           a.numTris == b.numTris && a.numMats == b.numMats && a.ldsScene == b.ldsScene && a.full == b.full &&
+           a.waveThreshold == b.waveThreshold && a.chunk == b.chunk && a.leafExit == b.leafExit &&
+           a.nodeExit == b.nodeExit && a.wide == b.wide && a.stackCap == b.stackCap && a.spillCap == b.spillCap &&
+           a.spill == b.spill && a.topBytes == b.topBytes && a.refBits == b.refBits && a.runOrder == b.runOrder &&
+           a.runCount == b.runCount && a.rngTable == b.rngTable && a.poolOffset == b.poolOffset &&
+           a.poolWords == b.poolWords && a.comb.format == b.comb.format;
+}
+
+// Makes batch `p` (its parameters otherwise complete, `blocks` its grid) the next batch of the open
+// run, or of a new run (the old one flushed first): the chain fields, the ring slot's scratch, and
+// the mailbox post.
+bool chain_batch(Ctx &c, hippt::MeshParams &p, long long blocks, long long option, const char **err) {
+    Ctx::Chain &ch = c.chain;
+    p.comb = hippt::CombineParams{c.accum, c.out, nullptr, p.bandPixels, p.totalItems, 0, p.frames, p.comb.format};
+    bool same = ch.live && blocks == ch.blocks && chain_same(p, ch.key);
+    if (same && ch.seq == 1) {  // the run's frame pattern: every batch the same frames, or the next ones
+        const int d = p.firstFrame - ch.firstFrame;
+        if (d == 0 || d == p.frames)
+            ch.step = d;
+        else
+            same = false;
+    } else if (same && p.firstFrame != ch.firstFrame + int(ch.seq) * ch.step) {
+        same = false;
+    }
+    if (!same) {
+        if (!flush_deferred(c, err)) return false;  // the old run's (or an unchained batch's) combines
+        unsigned shift = 6;
+        while ((1u << shift) < p.totalItems) ++shift;
+        const unsigned cap = chain_cap(option, p.totalItems);
+        unsigned slots = 2;
+        while (slots < 2 * cap) slots <<= 1;
+        slots = std::min(slots, hippt::kChainSlotsMax);
+        const size_t bytes = (size_t(slots) << shift) * 3 * sizeof(float);
+        if (!c.chainCtl) HIP_TRY(hipMalloc(&c.chainCtl, hippt::kChainCtlWords * sizeof(unsigned)));
+        if (!c.chainBox) {
+            HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c.chainBox), sizeof(unsigned long long),
+                                  hipHostMallocMapped | hipHostMallocCoherent));
+            *c.chainBox = 0;
+            void *d = nullptr;
+            HIP_TRY(hipHostGetDevicePointer(&d, c.chainBox, 0));
+            c.chainBoxDev = static_cast<unsigned long long *>(d);
+        }
+        if (c.chainScratchBytes < bytes) {
+            HIP_TRY(hipStreamSynchronize(c.stream));
+            (void)hipFree(c.chainScratch);
+            c.chainScratch = nullptr;
+            c.chainScratchBytes = 0;
+            HIP_TRY(hipMalloc(&c.chainScratch, bytes));
+            c.chainScratchBytes = bytes;
+        }
+        HIP_TRY(hipMemsetAsync(c.chainCtl, 0, hippt::kChainCtlWords * sizeof(unsigned), c.stream));
+        ch.live = true;
+        ch.run = (ch.run + 1u) & 0x7fffffffu;
+        ch.seq = 0;
+        ch.epoch = 0;
+        ch.firstFrame = p.firstFrame;
+        ch.step = -1;
+        ch.slots = slots;
+        ch.shift = shift;
+        ch.cap = cap;
+        ch.blocks = blocks;
+        p.comb.scratch = c.chainScratch;
+        p.comb.firstFrame = p.firstFrame;
+        ch.key = p;
+    }
+    p.scratch = c.chainScratch;
+    p.queue = c.chainCtl;
+    p.combCtr = nullptr;
+    p.comb.scratch = c.chainScratch;
+    p.comb.firstFrame = ch.firstFrame;
+    p.chainCtl = c.chainCtl;
+    p.chainBox = c.chainBoxDev;
+    p.chainSeq = ch.seq;
+    p.chainEpoch = ch.epoch;
+    p.chainRun = ch.run;
+    p.chainSlots = ch.slots;
+    p.chainShift = ch.shift;
+    p.chainCap = ch.cap;
+    p.chainStep = ch.step;
+    // post: one word, so that a launch reads the run, its frame pattern and the last batch together
+    const unsigned long long consecutive = ch.step > 0 ? 1u : 0u;
+    __atomic_store_n(c.chainBox, ((unsigned long long)ch.run << 33) | (consecutive << 32) | ch.seq, __ATOMIC_RELEASE);
+    ++ch.seq;
+    ++ch.epoch;
+    c.hostSamples += p.totalItems;
     return true;
 }
 
@@ -1122,6 +1294,10 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                                                                      spills, topBytes, lm, poolWords);
                     c.meshBlocksPerCu[1] = hippt::mesh_blocks_per_cu(true, s.scene.full, fmt, stackDepth, ln, lt,
                                                                      spills, topBytes, lm, poolWords);
+                    c.meshBlocksPerCuChain = poolWords && fmt == hippt::kWideFloat
+                                                 ? hippt::mesh_blocks_per_cu(false, s.scene.full, fmt, stackDepth, ln,
+                                                                             lt, spills, topBytes, lm, poolWords, true)
+                                                 : 0;
                     c.occKey = occKey;
                 }
                 s.activeTopBytes = topBytes;
@@ -1132,9 +1308,16 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                     const unsigned total = bandPixels * unsigned(nf);
                     // the megakernel takes the previous batch's combine along; other batches flush it
                     const bool fuse = maxDepth > 0 && s.pathMode == 0 && s.fuseCombine != 0;
+                    // chained batches (Ctx::chain): asynchronous camera-pool megakernel batches over
+                    // 4-wide float nodes whose items fit the ring's slot bits
+                    const bool chained = fuse && !copy && !cnt && (s.chainBatches > 0 || (s.chainBatches < 0 && kChainAuto)) &&
+                                         poolWords != 0 &&
+                                         fmt == hippt::kWideFloat && c.meshBlocksPerCuChain > 0 &&
+                                         total <= (1u << hippt::kChainMaxShift);
+                    if ((!fuse || !chained) && !flush_chain(c, err)) return false;
                     if (!fuse && !flush_deferred(c, err)) return false;
                     float *scratch = nullptr;
-                    if (!batch_scratch(c, need, &scratch, err)) return false;
+                    if (!chained && !batch_scratch(c, need, &scratch, err)) return false;
                     if (maxDepth <= 0) {
                         // ray_color with depth <= 0 returns black without tracing (RayTracer.h:582-583)
                         HIP_TRY(hipMemsetAsync(scratch, 0, size_t(total) * 3 * sizeof(float), c.stream));
@@ -1218,16 +1401,22 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         if (s.pathMode == 1) {
                             if (!run_wavefront(c, p, cnt, spills, s.scene.stackBound4 + 3, err)) return false;
                         } else {
-                            long long blocks = (long long)c.cus * bpc;
+                            long long blocks =
+                                (long long)c.cus * (chained && s.blocksPerCu <= 0 ? c.meshBlocksPerCuChain : bpc);
                             blocks = std::min<long long>(blocks, (total + hippt::kMeshBlock - 1) / hippt::kMeshBlock);
                             blocks = std::max<long long>(blocks, 1);
                             if (!ensure_spill(c, p, blocks, spills, s.scene.stackBound4 + 3, err)) return false;
-                            HIP_TRY(hipMemsetAsync(c.queue, 0, kQueueBytes, c.stream));
-                            if (c.hasDeferred) {
-                                p.comb = c.deferred;
-                                c.hasDeferred = false;
+                            if (chained) {
+                                p.comb.format = s.pixelFormat;
+                                if (!chain_batch(c, p, blocks, s.chainBatches, err)) return false;
+                            } else {
+                                HIP_TRY(hipMemsetAsync(c.queue, 0, kQueueBytes, c.stream));
+                                if (c.hasDeferred) {
+                                    p.comb = c.deferred;
+                                    c.hasDeferred = false;
+                                }
+                                p.combCtr = c.queue + kCombCtrWord;
                             }
-                            p.combCtr = c.queue + kCombCtrWord;
                             EventPair ev;
                             if (!next_events(c, ev, err)) return false;
                             HIP_TRY(hipEventRecord(ev.a, c.stream));
@@ -1236,6 +1425,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                             c.pending.push_back({0, ev});
                         }
                     }
+                    if (chained && maxDepth > 0) continue;  // its combine belongs to the run (Ctx::chain)
                     c.deferred = hippt::CombineParams{c.accum, c.out, scratch, bandPixels, total, firstFrame + b, nf,
                                                       s.pixelFormat};
                     c.hasDeferred = true;
@@ -1798,7 +1988,7 @@ extern "C" bool hipptGetStats(hipptStats *out) try {
         unsigned long long v[kStatWords];
         if (!read_stats(c, v)) return false;
         out->segments += v[0];
-        out->pixelSamples += v[1];
+        out->pixelSamples += v[1] + c.hostSamples;
         out->nodeVisits += v[2];
         out->triTests += v[3];
     }
@@ -1828,6 +2018,7 @@ extern "C" int hipptGetCounters(unsigned long long *out, int n) try {
     for (Ctx &c : s.ctxs) {
         unsigned long long v[kStatWords];
         if (!read_stats(c, v)) return 0;
+        v[1] += c.hostSamples;
         for (int i = 0; i < n; ++i) out[i] += v[i];
     }
     return n;
@@ -1845,6 +2036,7 @@ extern "C" void hipptResetStats(void) try {
     for (Ctx &c : s.ctxs) {
         (void)hipSetDevice(c.device);
         (void)hipMemset(c.stats, 0, kStatBytes);
+        c.hostSamples = 0;
     }
     s.traceMs = s.combineMs = 0;
     s.traceLaunches = s.combineLaunches = 0;
@@ -1962,6 +2154,10 @@ extern "C" bool hipptSetOption(int key, long long value) try {
         if (value != -1 && value != 0 && value != 3 && value != 6) return false;
         s.wfSort = int(value);
         return true;
+    case HIPPT_OPT_CHAIN:
+        if (value < -1 || value > 8) return false;
+        s.chainBatches = int(value);
+        return true;
     default: return false;
     }
 } catch (const std::exception &e) {
@@ -2011,6 +2207,7 @@ extern "C" long long hipptGetOption(int key) try {
     case HIPPT_OPT_FUSE_COMBINE: return s.fuseCombine;
     case HIPPT_OPT_ITEM_ORDER: return s.itemOrder;
     case HIPPT_OPT_WAVEFRONT_SORT: return s.wfSort;
+    case HIPPT_OPT_CHAIN: return s.chainBatches;
     case HIPPT_INFO_LDS_TOP_BYTES: return s.activeTopBytes;
     case HIPPT_INFO_BLOCKS_PER_CU: return s.activeBlocksPerCu;
     default: return -1;

@@ -109,6 +109,49 @@ struct MeshParams {
     // claimed from *combCtr (zeroed with the work queue)
     CombineParams comb;
     unsigned *combCtr;
+    // Chained batches (chainCtl non-null; hippt_trace.h "chained batches").  A run is a
+    // sequence of asynchronous batches with the same scene, camera, rows and frames per batch, each
+    // rendering the same frames again or the next ones; batch t of the run (t = 0, 1, ...) has ring
+    // slot t % chainSlots: its work counters are the slot's block of chainCtl, its radiances start
+    // at sample slot << chainShift of `scratch`, and its items carry the slot above bit chainShift
+    // (so store_radiance is unchanged).  This launch is the run's launch number chainEpoch and was
+    // enqueued for batch chainSeq; it combines every batch that earlier launches finished and did not
+    // combine, then traces from the first batch no launch has taken, going on with the later batches
+    // the host has posted (*chainBox = run << 33 | consecutive frames << 32 | last posted batch) up to
+    // chainCap batches and the ring's free slots.  comb.* (frames, bandPixels, format, accum, out)
+    // describe every batch of the run; comb.firstFrame is batch 0's first frame and chainStep the
+    // frames from one batch to the next (-1: not known when enqueued; read from the mailbox).
+    unsigned *chainCtl;
+    const unsigned long long *chainBox;
+    unsigned chainSeq, chainEpoch, chainRun;
+    unsigned chainSlots, chainShift, chainCap;
+    int chainStep;
+};
+
+// Chained batches: the control block (unsigned words).  Ring slot k's block at k * kChainBlockWords:
+// the kQueues work counters 128 B apart, then (own line) a 64-bit marker (batch << 32 | launch + 1) of
+// the last launch that took a batch in this slot.  After the kChainSlotsMax blocks, at kChainCtlWord:
+// the first batch not yet combined after the launches of epoch parity 0 / 1 (+0 / +32), the combine
+// chunk counters of epoch parity 0 / 1 (+64 / +96).
+constexpr unsigned kChainSlotsMax = 16, kChainBlockWords = 8 * 32 + 32, kChainMarkerWord = 8 * 32;
+constexpr unsigned kChainCtlWord = kChainSlotsMax * kChainBlockWords, kChainCtlWords = kChainCtlWord + 224;
+// (+128: a device copy of the host mailbox word, 64-bit; +160: the realtime stamp of its last
+// completed refresh; +192: the stamp of the last claimed refresh)
+constexpr unsigned kChainBoxCacheWord = kChainCtlWord + 128, kChainBoxStampWord = kChainCtlWord + 160,
+                   kChainBoxClaimWord = kChainCtlWord + 192;
+// batches of at most 2^kChainMaxShift items chain (the slot bits above them, kNone above all)
+constexpr unsigned kChainMaxShift = 27;
+// camera-pool kernels: per-wave state words in LDS before each wave's pool (trace::WaveWords)
+constexpr unsigned kWaveWords = 16;
+
+// The chain's final combine (launch_chain_flush): every batch of the run that no launch combined,
+// [first uncombined (from the control block, launch epoch `epoch`), lastSeq], in order per pixel.
+struct ChainFlushParams {
+    CombineParams comb;  // as MeshParams::comb (comb.firstFrame: batch 0's first frame)
+    const float *scratch;
+    const unsigned *ctl;
+    unsigned epoch, lastSeq, slots, shift;
+    int step;
 };
 
 
@@ -131,6 +174,7 @@ inline hipError_t check_lds_at_zero(const void *kernel) {
 hipError_t launch_sphere4(const Sphere4Params &p, hipStream_t s);
 hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hipStream_t s);
 hipError_t launch_combine(const CombineParams &p, hipStream_t s, const HostFrame &h = HostFrame{});
+hipError_t launch_chain_flush(const ChainFlushParams &p, hipStream_t s);
 // random_in_unit_sphere's rejection loop (RayTracer.h:155-161 with the hash RNG and the short-cycle
 // escape) is a pure function of the RNG state it starts from: table[s] = the state from which the
 // accepted candidate's three draws are made.  One 32-bit word per state: 16 GiB.
@@ -138,7 +182,8 @@ constexpr size_t kRngTableBytes = size_t(4) << 32;
 hipError_t launch_rng_table(uint32_t *table, hipStream_t s);
 // Resident mesh-kernel blocks per CU for a given LDS stack depth and LDS scene size.
 int mesh_blocks_per_cu(bool countTraversal, bool full, int fmt, int stackDepth, int ldsNodes, int ldsTris, bool spill,
-                       unsigned topBytes = 0, int ldsMats = 0, int poolWords = 0);
+                       unsigned topBytes = 0, int ldsMats = 0, int poolWords = 0, bool chain = false);
+// (poolWords != 0: each wave's pool block also holds its kWaveWords state words)
 size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide, unsigned topBytes = 0, int ldsMats = 0,
                       int poolWords = 0);
 // camera-ray pool words per ray: item, rng, direction (+ origin unless every ray starts at the

@@ -263,6 +263,53 @@ __device__ __forceinline__ bool combine_chunk(const MeshParams &P) {
     return true;
 }
 
+// Chained batches (hippt_trace.h): the running average of band pixel p over the run's batches
+// [c0, c1] in order (batch b: frames C.firstFrame + b*step + fl, its samples in ring slot b % slots).
+template <int UNROLL, bool HOST = false>
+__device__ __forceinline__ void combine_pixel_chain(const CombineParams &C, const float *scratch, unsigned p, int c0,
+                                                    int c1, unsigned slots, unsigned shift, int step,
+                                                    const HostFrame &H = HostFrame{}) {
+    float4 acc = C.accum[p];
+    for (int b = c0; b <= c1; ++b) {
+        const float *scr = scratch + 3 * ((size_t(unsigned(b) & (slots - 1u)) << shift) + p);
+        const int f0 = C.firstFrame + b * step;
+#pragma unroll UNROLL
+        for (int fl = 0; fl < C.frames; ++fl) {
+            const float3 L = *reinterpret_cast<const float3 *>(scr + 3 * size_t(fl) * C.bandPixels);
+            const float ff = float(f0 + fl), fc = float(f0 + fl + 1);
+            acc.x = fmaf(acc.x, ff, L.x) / fc;
+            acc.y = fmaf(acc.y, ff, L.y) / fc;
+            acc.z = fmaf(acc.z, ff, L.z) / fc;
+        }
+    }
+    acc.w = 1.0f;
+    C.accum[p] = acc;
+    const uint32_t word = pack_pixel(acc.x, acc.y, acc.z, C.format);
+    C.out[p] = word;
+    if (HOST && H.host) {
+        const unsigned yb = p / unsigned(H.width), x = p - yb * unsigned(H.width);
+        H.host[size_t(unsigned(H.y0) + yb * unsigned(H.stride)) * unsigned(H.width) + x] = word;
+    }
+}
+
+// combine_chunk of a CHAIN launch: 64 pixels over its combine range (ChainWave::c0..c1), chunks from
+// the launch's epoch-parity counter; arguments loaded where they are used.
+__device__ __forceinline__ bool combine_chunk_chain(const ChainWave *cw) {
+    unsigned *const ctl = late_field(chainCtl);
+    const unsigned e = late_field(chainEpoch);
+    const unsigned bandPixels = late_field(comb.bandPixels);
+    unsigned base = 0;
+    if (__lane_id() == 0) base = atomicAdd(ctl + kChainCtlWord + 64u + 32u * (e & 1u), 64u);
+    base = __builtin_amdgcn_readfirstlane(base);
+    if (base >= bandPixels) return false;
+    const unsigned p = base + __lane_id();
+    if (p < bandPixels)
+        combine_pixel_chain<8>(late_field(comb), late_field(scratch), p, int(__builtin_amdgcn_readfirstlane(cw->c0)),
+                               int(__builtin_amdgcn_readfirstlane(cw->c1)), late_field(chainSlots),
+                               late_field(chainShift), max(0, late_field(chainStep)));
+    return true;
+}
+
 // Camera-ray pool (POOL, HIPPT_OPT_CAMERA_POOL): a refill happens when a lane's path ends, so only
 // the lanes whose paths ended together generate camera rays, at ~30% SIMD efficiency (Cornell,
 // tools/phase_profile.py).  With the pool, the wave generates the camera rays of its next 64 work
@@ -291,10 +338,12 @@ __device__ __forceinline__ void pool_take(const MeshParams &P, const float *pool
     }
 }
 
+// CHAIN: chained batches (hippt_trace.h; camera-pool kernels over 4-wide float nodes only)
 template <bool STATS, bool LDS_SCENE, bool FULL, bool WIDE, bool QUANT, bool SPILL = true, bool POOL = false,
-          bool HYBRID = false, bool HALF = false>
+          bool HYBRID = false, bool HALF = false, bool CHAIN = false>
 __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_EU : HIPPT_MESH_WAVES_PER_EU) HIPPT_SGPR_ATTR void mesh_kernel(MeshParams P) {
     static_assert(!QUANT || (WIDE && !LDS_SCENE), "quantized nodes: 4-wide global-memory traversal only");
+    static_assert(!CHAIN || (POOL && WIDE && !QUANT && !HYBRID && !HALF && !STATS), "chained batches: pool kernels");
 #ifdef HIPPT_DEBUG_TIMELINE
     const unsigned tlw = blockIdx.x * 4u + (threadIdx.x >> 6);
     unsigned long long tlDrained = 0, tlItems = 0, tlRounds = 0, tlLate = 0;
@@ -363,13 +412,25 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     constexpr int nodeF4 = LDS_SCENE ? ldsNodeF4 : (WIDE ? (QUANT ? 4 : 8) : 4);
     const SpillArea S{P.spill, (blockIdx.x * unsigned(kMeshBlock) + threadIdx.x) * unsigned(P.spillCap), P.stackCap};
 
-    // this wave's camera-ray pool (POOL): entries [poolNext, 64) not taken yet (wave-uniform)
+    // this wave's camera-ray pool (POOL): entries [poolNext, 64) not taken yet (wave-uniform).  Each
+    // wave's pool block starts with its kWaveWords state words (WaveWords: work queue, segment count,
+    // chain state), so that their address is the pool's minus a constant.
+    constexpr unsigned kWW = POOL ? kWaveWords : 0u;
     float *const pool = reinterpret_cast<float *>(reinterpret_cast<char *>(lds) + P.poolOffset) +
-                        (threadIdx.x >> 6) * unsigned(P.poolWords * 64);
+                        (threadIdx.x >> 6) * unsigned(P.poolWords * 64 + kWW) + kWW;
     unsigned poolNext = 64;
-
+    WaveWords *const ww = reinterpret_cast<WaveWords *>(pool - kWW);
+    ChainWave *const cw = &ww->cw;
+    // CHAIN kernels keep the work queue and the segment count in LDS (ww->Q, ww->segs), the others in
+    // registers
     WorkQueue Q;
-    queue_begin(Q, P.totalItems, P.chunk);
+    if constexpr (CHAIN) {
+        chain_begin(Q, cw);
+        store_queue(&ww->Q, Q);
+        if (__lane_id() == 0) ww->segs = 0;
+    } else {
+        queue_begin(Q, P.totalItems, P.chunk);
+    }
     unsigned item = kNone;
     uint32_t rng = 0;
     int depth = 0;
@@ -407,9 +468,10 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     unsigned long long rtRounds = 0, rtLive = 0;
     auto rt_flush = [&](unsigned nb) {
         const unsigned long long a = wave_sum((unsigned long long)(samples - rtSamples0));
-        const unsigned long long b = wave_sum((unsigned long long)(segs - rtSegs0));
+        const unsigned wsegs = CHAIN ? __builtin_amdgcn_readfirstlane(ww->segs) : 0u;
+        const unsigned long long b = CHAIN ? (unsigned long long)(wsegs - rtSegs0) : wave_sum((unsigned long long)(segs - rtSegs0));
         rtSamples0 = samples;
-        rtSegs0 = segs;
+        rtSegs0 = CHAIN ? wsegs : segs;
         if (__lane_id() == 0) {
             const unsigned k = ((blockIdx.x * 4u + (threadIdx.x >> 6)) % unsigned(kRateSlots) * unsigned(kRateBuckets) +
                                 min(rtBucket, unsigned(kRateBuckets - 1))) * 5u;
@@ -424,9 +486,11 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     };
 #endif
     unsigned waveThr = unsigned(P.waveThreshold);
-    bool combLeft = P.comb.bandPixels != 0;
+    bool combLeft = CHAIN ? int(__builtin_amdgcn_readfirstlane(cw->c1)) >= int(__builtin_amdgcn_readfirstlane(cw->c0))
+                          : P.comb.bandPixels != 0;
+    auto comb_step = [&]() { return CHAIN ? combine_chunk_chain(cw) : combine_chunk(P); };
     if (combLeft && (blockIdx.x & 1u) == 0 && threadIdx.x < 64u)
-        while (combLeft) combLeft = combine_chunk(P);
+        while (combLeft) combLeft = comb_step();
     for (;;) {
         prof<STATS>(pc, 0);
 #ifdef HIPPT_DEBUG_TIMELINE
@@ -454,21 +518,53 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                 }
                 if (n > avail) {
                     // the camera rays of the wave's next 64 items, every lane at once
-                    const unsigned it = HIPPT_LATE_CAM ? order_item_late(queue_fetch(true, Q, P.queue, P.totalItems, P.chunk))
-                                                       : order_item(P, queue_fetch(true, Q, P.queue, P.totalItems, P.chunk));
+                    unsigned it;
+                    Ray c{};
+                    uint32_t crng = 0;
+                    if constexpr (CHAIN) {
+                        // items of the wave's batch (ChainWave::t); a drained batch moves the wave into
+                        // the run's next one (chain_next) and the lanes still without an item take its
+                        // items, so that a refill spans batches and no lane waits for a batch's end
+                        WorkQueue Q = load_queue(&ww->Q);
+                        unsigned raw = kNone, tItem = 0;
+                        bool want = true;
+                        for (;;) {
+                            const unsigned t = __builtin_amdgcn_readfirstlane(cw->t);
+                            const unsigned got =
+                                queue_fetch(want, Q, chain_block(late_field(chainCtl), t, late_field(chainSlots)),
+                                            late_field(totalItems), late_field(chunk),
+                                            t == __builtin_amdgcn_readfirstlane(cw->stat));
+                            if (want && got != kNone) {
+                                raw = got;
+                                tItem = t;
+                                want = false;
+                            }
+                            if (!__ballot(want) || !chain_next(Q, cw)) break;
+                        }
+                        store_queue(&ww->Q, Q);
+                        it = order_item_late(raw);
+                        if (it != kNone) {
+                            // the item's frames: its batch's offset from the launch's own batch's
+                            const int step = int(__builtin_amdgcn_readfirstlane(unsigned(cw->step)));
+                            camera_sample(cam_args_late(), it, c, crng,
+                                          (tItem - late_field(chainSeq)) * unsigned(max(step, 0)));
+                            it |= (tItem & (late_field(chainSlots) - 1u)) << late_field(chainShift);
+                        }
+                    } else {
+                        it = HIPPT_LATE_CAM ? order_item_late(queue_fetch(true, Q, P.queue, P.totalItems, P.chunk))
+                                            : order_item(P, queue_fetch(true, Q, P.queue, P.totalItems, P.chunk));
+                        if (it != kNone) {
+                            if (HIPPT_LATE_CAM)
+                                camera_sample(cam_args_late(), it, c, crng);
+                            else
+                                camera_sample(P, it, c, crng);
+                        }
+                    }
 #ifdef HIPPT_DEBUG_TIMELINE
                     if (!tlDrained && __ballot(it == kNone)) tlDrained = __builtin_amdgcn_s_memrealtime();
                     tlItems += __popcll(__ballot(it != kNone));
 #endif
-                    Ray c{};
-                    uint32_t crng = 0;
-                    if (it != kNone) {
-                        prof<STATS>(pc, 1);
-                        if (HIPPT_LATE_CAM)
-                            camera_sample(cam_args_late(), it, c, crng);
-                        else
-                            camera_sample(P, it, c, crng);
-                    }
+                    if (it != kNone) prof<STATS>(pc, 1);
                     const unsigned k = __lane_id();
                     pool[k] = __uint_as_float(it);
                     pool[64 + k] = __uint_as_float(crng);
@@ -537,10 +633,16 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         } while (__popcll(__ballot(busy(T))) > (FINISH ? waveThr : unsigned(P.waveThreshold)));
 
         // ---- shading: lanes whose traversal finished (ray_color step, RayTracer.h:579-596) ----
+        // (a lane resuming a pending draw continues its segment; CHAIN kernels count the wave's
+        // segments in ww->segs, one LDS add per round)
+        if constexpr (CHAIN) {
+            const unsigned long long sm = __ballot(item != kNone && !busy(T) && !(CAP && pend != 0u));
+            if (__lane_id() == 0 && sm) atomicAdd(&ww->segs, unsigned(__popcll(sm)));
+        }
         if (item != kNone && !busy(T)) {
             prof<STATS>(pc, 6);
             const bool cont = CAP && pend != 0u;  // resumes a pending draw: same segment
-            if (!cont) ++segs;
+            if (!CHAIN && !cont) ++segs;
             bool finished = false;
             float Lr = 0.0f, Lg = 0.0f, Lb = 0.0f;
             if (!FULL) {
@@ -584,7 +686,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
             }
             if (finished) {
                 store_radiance(P.scratch, item, Lr, Lg, Lb);
-                ++samples;
+                if (!CHAIN) ++samples;  // (CHAIN batches: every item is one sample, counted by the host)
 #ifdef HIPPT_DEBUG_TIMELINE
                 if (tlDrained) ++tlLate;
 #endif
@@ -593,8 +695,14 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
             }
         }
     }
-
-    while (combLeft) combLeft = combine_chunk(P);
+    while (combLeft) combLeft = comb_step();
+    if (CHAIN && __lane_id() == 0) {
+        // for the next launch: the first batch not combined after this one (ChainWave::c0..c1 done)
+        const int c0 = int(cw->c0), c1 = int(cw->c1);
+        unsigned *const ctl = late_field(chainCtl);
+        __hip_atomic_store(ctl + kChainCtlWord + 32u * (late_field(chainEpoch) & 1u), unsigned(max(c0, c1 + 1)),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
 #ifdef HIPPT_DEBUG_RATE
     rt_flush(0);
 #endif
@@ -608,7 +716,8 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         g_timeline[8 * tlw + 7] = tlLate;    // samples lane 0 finished after that
     }
 #endif
-    const unsigned long long segsW = wave_sum(segs), samplesW = wave_sum(samples);
+    const unsigned long long segsW = CHAIN ? (unsigned long long)__builtin_amdgcn_readfirstlane(ww->segs) : wave_sum(segs);
+    const unsigned long long samplesW = CHAIN ? 0ull : wave_sum(samples);
     if (STATS) {
         nvis = wave_sum(nvis);
         ntest = wave_sum(ntest);
@@ -635,6 +744,17 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
 __global__ __launch_bounds__(256) void combine_kernel(CombineParams P, HostFrame H) {
     const unsigned stride = gridDim.x * 256u;
     for (unsigned p = blockIdx.x * 256u + threadIdx.x; p < P.bandPixels; p += stride) combine_pixel<8, true>(P, p, H);
+}
+
+// The chain's final combine (ChainFlushParams): every batch of the run no launch combined, in order.
+__global__ __launch_bounds__(256) void chain_flush_kernel(ChainFlushParams P) {
+    const int c0 = int(__hip_atomic_load(P.ctl + kChainCtlWord + 32u * ((P.epoch + 1u) & 1u), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT));
+    const int c1 = int(P.lastSeq);
+    if (c1 < c0) return;
+    const unsigned stride = gridDim.x * 256u;
+    for (unsigned p = blockIdx.x * 256u + threadIdx.x; p < P.comb.bandPixels; p += stride)
+        combine_pixel_chain<8>(P.comb, P.scratch, p, c0, c1, P.slots, P.shift, P.step);
 }
 
 // table[s] for s = 0 .. 2^32-1: the state from which random_in_unit_sphere, entered with state s,
@@ -707,7 +827,8 @@ size_t mesh_lds_bytes(int stackDepth, int ldsNodes, int ldsTris, bool wide, unsi
                       int poolWords) {
     return size_t(stackDepth + 1) * kMeshBlock * sizeof(int) +
            size_t(ldsNodes) * (wide ? kLdsNode4F4 : kLdsNodeF4) * 16 + size_t(ldsTris) * (3 + 1) * 16 + topBytes +
-           size_t(ldsMats) * 2 * 16 + size_t(poolWords) * kMeshBlock * sizeof(float);
+           size_t(ldsMats) * 2 * 16 +
+           (poolWords ? (size_t(poolWords) * 64 + kWaveWords) * (kMeshBlock / 64) * sizeof(float) : 0);
 }
 
 size_t mesh_lds_scene_limit() { return 24u << 10; }
@@ -740,7 +861,18 @@ static MeshFn mesh_fn_fmt(bool lds, int fmt, bool spill, bool pool) {
         return pool ? mesh_fn_wide<STATS, FULL, true, true>(lds, fmt) : mesh_fn_wide<STATS, FULL, true, false>(lds, fmt);
     return pool ? mesh_fn_wide<STATS, FULL, false, true>(lds, fmt) : mesh_fn_wide<STATS, FULL, false, false>(lds, fmt);
 }
-static MeshFn mesh_fn(bool count, bool lds, bool full, int fmt, bool spill, bool pool) {
+// chained batches (MeshParams::chainCtl): the timed camera-pool kernels over 4-wide float nodes
+template <bool FULL, bool SPILL>
+static MeshFn mesh_fn_chain(bool lds) {
+    return lds ? mesh_kernel<false, true, FULL, true, false, SPILL, true, false, false, true>
+               : mesh_kernel<false, false, FULL, true, false, SPILL, true, false, false, true>;
+}
+static MeshFn mesh_fn(bool count, bool lds, bool full, int fmt, bool spill, bool pool, bool chain = false) {
+    if (chain) {
+        if (count || fmt != kWideFloat || !pool) return nullptr;
+        if (full) return spill ? mesh_fn_chain<true, true>(lds) : mesh_fn_chain<true, false>(lds);
+        return spill ? mesh_fn_chain<false, true>(lds) : mesh_fn_chain<false, false>(lds);
+    }
     if (count)
         return full ? mesh_fn_fmt<true, true>(lds, fmt, spill, pool) : mesh_fn_fmt<true, false>(lds, fmt, spill, pool);
     return full ? mesh_fn_fmt<false, true>(lds, fmt, spill, pool) : mesh_fn_fmt<false, false>(lds, fmt, spill, pool);
@@ -760,10 +892,17 @@ hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hip
     const bool pool = p.poolWords != 0;
     if (pool && ((p.wide != kWideFloat && p.wide != kWideHalf) || (p.poolWords != kPoolWordsPinhole && p.poolWords != kPoolWordsFull)))
         return hipErrorInvalidValue;
+    const bool chain = p.chainCtl != nullptr;
+    if (chain && (!p.chainBox || p.chainSlots < 2 || p.chainSlots > kChainSlotsMax || (p.chainSlots & (p.chainSlots - 1)) ||
+                  p.chainShift > kChainMaxShift || p.totalItems > (1u << p.chainShift) || p.chainCap < 1 ||
+                  p.chainCap >= p.chainSlots || p.comb.bandPixels != p.bandPixels || p.comb.frames != p.frames))
+        return hipErrorInvalidValue;
     const size_t bytes = mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0, p.wide != 0, p.topBytes,
                                         lds ? p.numMats : 0, p.poolWords);
-    if (pool && p.poolOffset != bytes - size_t(p.poolWords) * kMeshBlock * sizeof(float)) return hipErrorInvalidValue;
-    const MeshFn fn = mesh_fn(countTraversal, lds, p.full != 0, p.wide, p.spill != nullptr, pool);
+    if (pool && p.poolOffset != bytes - (size_t(p.poolWords) * 64 + kWaveWords) * (kMeshBlock / 64) * sizeof(float))
+        return hipErrorInvalidValue;
+    const MeshFn fn = mesh_fn(countTraversal, lds, p.full != 0, p.wide, p.spill != nullptr, pool, chain);
+    if (!fn) return hipErrorInvalidValue;
     if (p.wide && (lds || p.topBytes || pool)) {
         const hipError_t e = check_lds_at_zero(reinterpret_cast<const void *>(fn));
         if (e != hipSuccess) return e;
@@ -780,14 +919,25 @@ hipError_t launch_combine(const CombineParams &p, hipStream_t s, const HostFrame
     return hipGetLastError();
 }
 
+hipError_t launch_chain_flush(const ChainFlushParams &p, hipStream_t s) {
+    if (p.comb.bandPixels == 0) return hipSuccess;
+    if (!p.ctl || p.slots < 2 || p.slots > kChainSlotsMax || (p.slots & (p.slots - 1)) || p.shift > kChainMaxShift)
+        return hipErrorInvalidValue;
+    unsigned blocks = (p.comb.bandPixels + 255u) / 256u;
+    if (blocks > 8192u) blocks = 8192u;
+    hipLaunchKernelGGL(chain_flush_kernel, dim3(blocks), dim3(256), 0, s, p);
+    return hipGetLastError();
+}
+
 int mesh_blocks_per_cu(bool countTraversal, bool full, int fmt, int stackDepth, int ldsNodes, int ldsTris, bool spill,
-                       unsigned topBytes, int ldsMats, int poolWords) {
+                       unsigned topBytes, int ldsMats, int poolWords, bool chain) {
     int n = 0;
     const bool lds = ldsNodes > 0;
     const size_t bytes = mesh_lds_bytes(stackDepth, ldsNodes, ldsTris, fmt != kWide2, topBytes, ldsMats, poolWords);
-    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(
-        &n, mesh_fn(countTraversal, lds, full, lds && fmt >= kWideQuant ? kWideFloat : fmt, spill, poolWords != 0),
-        kMeshBlock, bytes);
+    const MeshFn fn = mesh_fn(countTraversal, lds, full, lds && fmt >= kWideQuant ? kWideFloat : fmt, spill,
+                              poolWords != 0, chain);
+    if (!fn) return 1;
+    hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, kMeshBlock, bytes);
     if (e != hipSuccess || n <= 0) n = 1;
     // the query ignores the trap handler's SGPRs (kMaxResidentBlocks): a larger persistent grid
     // leaves blocks waiting for a slot until others finish

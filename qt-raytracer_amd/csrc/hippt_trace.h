@@ -179,9 +179,10 @@ __device__ __forceinline__ void queue_begin(WorkQueue &Q, unsigned total, unsign
 }
 
 // One item per requesting lane (kNone once every queue is drained).  Whole wave, uniform
-// control flow; the pool and queue state are wave-uniform.
+// control flow; the pool and queue state are wave-uniform.  stat: the queues have static first
+// chunks (queue_begin); a chained batch a launch moves into has none (chain_select).
 __device__ __forceinline__ unsigned queue_fetch(bool req, WorkQueue &Q, unsigned *ctr, unsigned total,
-                                                unsigned chunk) {
+                                                unsigned chunk, bool stat = true) {
     unsigned item = kNone;
     bool want = req;
     unsigned long long m = __ballot(want);
@@ -210,6 +211,7 @@ __device__ __forceinline__ unsigned queue_fetch(bool req, WorkQueue &Q, unsigned
             Q.next += min(unsigned(__popcll(m)), avail);
         } else if (--Q.left) {
             queue_select(Q, Q.g + 1 == kQueues ? 0u : Q.g + 1, total, chunk);
+            if (!stat) Q.dynBase = queue_start(total, Q.g);
             Q.next = Q.end = 0;
         }
     }
@@ -322,14 +324,207 @@ __device__ __forceinline__ unsigned order_item_late(unsigned it) {
     return run < runs ? order[fl * runs + run] + (q & 63u) : it;
 }
 
-// PP: MeshParams or CamArgs
+// ---- chained batches (MeshParams::chain*, CHAIN kernels) ----------------------------
+// One launch per asynchronous batch is still enqueued, but a launch whose batch is drained goes on with
+// the batches of its run the host has posted behind it, so that a run of batches pays the launch's
+// tail (the last paths finishing at falling lane use, ~0.2-0.3 ms) once per chainCap batches instead
+// of once per batch.  The rules that keep it exact:
+//  * a launch starts after the previous one on the stream has ended, so every batch before its own
+//    is finished, and so is every batch an earlier launch moved into (a wave leaves a batch only once
+//    all of its queues are drained, and a launch ends only when its waves have finished their paths):
+//    an earlier launch's marker in the batch's ring slot says so;
+//  * a launch combines (running average + tonemap, in frame order per pixel) every finished batch not
+//    yet combined, [c0, c1], beside its own tracing (the fused combine of one batch before), and
+//    records c1 + 1 for the next launch (by epoch parity: the next launch reads it, this one's late
+//    waves do not see it);
+//  * it traces from u = c1 + 1 (its own batch when no earlier launch took it: the first chunks then
+//    static, as unchained) up to min(c0 + slots - 1, u + chainCap - 1), so that it never writes a ring
+//    slot it combines or one a batch not yet combined holds; the host posts a batch in the mailbox
+//    before its launch is enqueued, and a launch takes a later batch only once the mailbox shows it;
+//  * the counters of the slots it combines are zeroed at its start for the batches that reuse them
+//    (no wave of the launch reads them: it traces only past c1);
+//  * the run's last combines are the final flush (launch_chain_flush), before anything reads or
+//    resets the image, and a new run starts from a zeroed control block.
+// Per wave, in LDS (WaveWords::cw):
+struct ChainWave {
+    unsigned t;         // the batch the wave's queue serves (its items carry its ring slot above chainShift)
+    unsigned spare;
+    unsigned tLim;      // the last batch this launch may trace
+    unsigned posted;    // batches before this one are known posted
+    int step;           // frames from one batch to the next (-1: not known yet)
+    unsigned c0, c1;    // this launch's combine range (c1 < c0: none)
+    unsigned stat;      // the batch whose queues have static first chunks (~0u: none)
+};
+// The camera-pool kernels' per-wave state kept in LDS between uses, kWaveWords words at the start of
+// each wave's pool block: the work queue (read and written back at each pool refill, once per 64
+// items), the wave's segment count and the chain state.  In registers they would be live across the
+// whole path loop, which has none to spare: the loop's peak is the node visit with every lane's path
+// state live, and the chained kernels spilled the path throughput to scratch until these moved out.
+struct WaveWords {
+    WorkQueue Q;
+    unsigned segs;
+    ChainWave cw;
+};
+static_assert(sizeof(WaveWords) == kWaveWords * 4, "per-wave LDS words");
+
+__device__ __forceinline__ WorkQueue load_queue(const WorkQueue *q) {
+    WorkQueue Q;
+    Q.g = __builtin_amdgcn_readfirstlane(q->g);
+    Q.left = __builtin_amdgcn_readfirstlane(q->left);
+    Q.next = __builtin_amdgcn_readfirstlane(q->next);
+    Q.end = __builtin_amdgcn_readfirstlane(q->end);
+    Q.qEnd = __builtin_amdgcn_readfirstlane(q->qEnd);
+    Q.dynBase = __builtin_amdgcn_readfirstlane(q->dynBase);
+    Q.waves = __builtin_amdgcn_readfirstlane(q->waves);
+    return Q;
+}
+__device__ __forceinline__ void store_queue(WorkQueue *q, const WorkQueue &Q) {
+    if (__lane_id() == 0) *q = Q;
+}
+
+#define late_field(f) late_arg_at<decltype(MeshParams::f)>(unsigned(offsetof(MeshParams, f)))
+
+__device__ __forceinline__ unsigned *chain_block(unsigned *ctl, unsigned t, unsigned slots) {
+    return ctl + (t & (slots - 1u)) * kChainBlockWords;
+}
+
+// Batch t taken by launch `epoch` (lane 0; every wave that moves into t stores the same word).
+__device__ __forceinline__ void chain_mark(unsigned *ctl, unsigned t, unsigned slots, unsigned epoch) {
+    if (__lane_id() == 0)
+        __hip_atomic_store(reinterpret_cast<unsigned long long *>(chain_block(ctl, t, slots) + kChainMarkerWord),
+                           ((unsigned long long)t << 32) | (epoch + 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// queue_select for a batch with (stat) or without static first chunks
+__device__ __forceinline__ void chain_select(WorkQueue &Q, unsigned g, unsigned total, unsigned chunk, bool stat) {
+    queue_select(Q, g, total, chunk);
+    if (!stat) Q.dynBase = queue_start(total, g);
+}
+
+// Kernel start of a CHAIN launch (whole wave): the combine range, the first batch to trace and the
+// wave's queue (static first chunk when that batch is the launch's own), state into *cw.
+__device__ __forceinline__ void chain_begin(WorkQueue &Q, ChainWave *cw) {
+    unsigned *const ctl = late_field(chainCtl);
+    const unsigned e = late_field(chainEpoch), own = late_field(chainSeq), R = late_field(chainSlots);
+    const unsigned total = late_field(totalItems), chunk = late_field(chunk);
+    unsigned c0 = 0;
+    if (__lane_id() == 0)
+        c0 = __hip_atomic_load(ctl + kChainCtlWord + 32u * ((e + 1u) & 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    c0 = __builtin_amdgcn_readfirstlane(c0);
+    // lane k: batch t0 + k finished by an earlier launch (its slot's marker), within the ring's window
+    const unsigned t0 = max(own, c0);
+    bool fin = false;
+    if (__lane_id() < R && t0 + __lane_id() < c0 + R) {
+        const unsigned t = t0 + __lane_id();
+        const unsigned long long m = __hip_atomic_load(
+            reinterpret_cast<const unsigned long long *>(chain_block(ctl, t, R) + kChainMarkerWord), __ATOMIC_RELAXED,
+            __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned by = unsigned(m);
+        fin = unsigned(m >> 32) == t && by != 0u && by <= e;
+    }
+    const unsigned nfin = unsigned(__builtin_ctzll(~__ballot(fin)));
+    // finished: every batch before the own one, and the run of marked batches from t0
+    const int c1 = max(int(t0 + nfin) - 1, int(own) - 1);
+    const unsigned u = unsigned(max(int(c0), c1 + 1));  // first batch to trace
+    const unsigned tLim = min(c0 + R - 1u, u + late_field(chainCap) - 1u);
+    const int step = late_field(chainStep);
+    if (__lane_id() == 0) {
+        cw->c0 = c0;
+        cw->c1 = unsigned(c1);
+        cw->tLim = tLim;
+        cw->posted = own + 1u;  // the own batch is posted before its launch is enqueued
+        cw->step = step;
+        cw->t = u == own ? own : u - 1u;
+        cw->stat = u == own ? own : ~0u;
+    }
+    if (u == own) {  // the own batch, untaken: first chunks static, as unchained
+        chain_mark(ctl, own, R, e);
+        queue_begin(Q, total, chunk);
+    } else {  // nothing to fetch: the wave's first loop ends at once and chain_next moves into batch u
+        Q.left = 0;
+        Q.next = Q.end = 0;
+    }
+    // this launch's bookkeeping for the next: block 0's first wave zeroes the next epoch's combine
+    // counter and the work counters of the slots combined here (their next batches' counters)
+    if (blockIdx.x == 0 && threadIdx.x < 64u) {
+        if (__lane_id() == 0)
+            __hip_atomic_store(ctl + kChainCtlWord + 64u + 32u * ((e + 1u) & 1u), 0u, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        for (int b = int(c0); b <= c1; ++b)
+            if (__lane_id() < kQueues)
+                __hip_atomic_store(chain_block(ctl, unsigned(b), R) + __lane_id() * kQueueStride, 0u, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// A wave whose batch is drained moves into the next batch of the run, if this launch may take it and
+// the mailbox shows it posted (whole wave; at a camera-pool refill, so that the lanes whose paths
+// ended take the next batch's items while the others go on with theirs).
+__device__ __forceinline__ bool chain_next(WorkQueue &Q, ChainWave *cw) {
+    const unsigned nt = __builtin_amdgcn_readfirstlane(cw->t) + 1u;
+    if (nt > __builtin_amdgcn_readfirstlane(cw->tLim)) return false;
+    int step = int(__builtin_amdgcn_readfirstlane(unsigned(cw->step)));
+    if (nt >= __builtin_amdgcn_readfirstlane(cw->posted)) {
+        // one 64-bit mailbox word: run << 33 | consecutive frames << 32 | last posted batch.  The host
+        // word is read over PCIe, and such reads serialise (~60 ns each: 7168 waves reaching their
+        // batch's end together waited 0.43 ms, r5d/r5e).  A device copy serves the launch's waves: a
+        // wave whose copy is not current refreshes it from the host only if the last refresh is older
+        // than kBoxRefresh ticks of the 100 MHz clock and it wins the refresh claim; a wave that loses
+        // the claim waits (bounded) for the winner's refresh to land.
+        constexpr unsigned long long kBoxRefresh = 1000;  // 10 us
+        unsigned lo = 0, hi = 0;
+        if (__lane_id() == 0) {
+            unsigned *const ctl0 = late_field(chainCtl);
+            auto *cache = reinterpret_cast<unsigned long long *>(ctl0 + kChainBoxCacheWord);
+            auto *stamp = reinterpret_cast<unsigned long long *>(ctl0 + kChainBoxStampWord);
+            auto *claim = reinterpret_cast<unsigned long long *>(ctl0 + kChainBoxClaimWord);
+            unsigned long long b = __hip_atomic_load(cache, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const unsigned run = late_field(chainRun);
+            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+            if (!(unsigned(b >> 33) == run && unsigned(b) >= nt) &&
+                now - __hip_atomic_load(stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= kBoxRefresh) {
+                const unsigned long long prev = atomicExch(claim, now);
+                if (now - prev >= kBoxRefresh) {  // this wave refreshes the copy
+                    b = __hip_atomic_load(late_field(chainBox), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    atomicMax(cache, b);  // (a run's words grow: run in the high bits, then the batch)
+                    __hip_atomic_store(stamp, now, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                } else {  // another wave's refresh (claimed at `prev`) is in flight
+                    for (unsigned k = 0; k < 4096u && __hip_atomic_load(stamp, __ATOMIC_ACQUIRE,
+                                                                         __HIP_MEMORY_SCOPE_AGENT) < prev; ++k)
+                        __builtin_amdgcn_s_sleep(2);
+                    b = __hip_atomic_load(cache, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                }
+            }
+            lo = unsigned(b);
+            hi = unsigned(b >> 32);
+        }
+        lo = __builtin_amdgcn_readfirstlane(lo);
+        hi = __builtin_amdgcn_readfirstlane(hi);
+        if ((hi >> 1) != late_field(chainRun) || nt > lo) return false;  // not (yet) posted, or a later run
+        step = (hi & 1u) ? late_field(frames) : 0;
+        if (__lane_id() == 0) {
+            cw->posted = lo + 1u;
+            cw->step = step;
+        }
+    }
+    unsigned *const ctl = late_field(chainCtl);
+    const unsigned R = late_field(chainSlots);
+    if (__lane_id() == 0) cw->t = nt;
+    chain_mark(ctl, nt, R, late_field(chainEpoch));
+    chain_select(Q, blockIdx.x % kQueues, late_field(totalItems), late_field(chunk), false);
+    Q.left = kQueues;
+    Q.next = Q.end = 0;
+    return true;
+}
+
+// PP: MeshParams or CamArgs.  frameAdd: a chained batch's frame offset from the launch's own frames.
 template <typename PP>
-__device__ __forceinline__ void camera_sample(const PP &P, unsigned it, Ray &r, uint32_t &rng) {
+__device__ __forceinline__ void camera_sample(const PP &P, unsigned it, Ray &r, uint32_t &rng, unsigned frameAdd = 0u) {
     unsigned fl, p, yb, x;
     divmod(it, P.bandPixels, P.rcpBandPixels, fl, p);
     divmod(p, unsigned(P.width), P.rcpWidth, yb, x);
     const unsigned y = unsigned(P.y0) + yb * unsigned(P.rowStride);
-    rng = pixel_seed(x, y, unsigned(P.width), unsigned(P.firstFrame) + fl);
+    rng = pixel_seed(x, y, unsigned(P.width), unsigned(P.firstFrame) + fl + frameAdd);
     const float s = (float(x) + rand01(rng)) * P.invW;
     const float t = (float(y) + rand01(rng)) * P.invH;
     float qx, qy;

@@ -53,6 +53,7 @@ OPT_CAMERA_POOL = 26
 OPT_FUSE_COMBINE = 27
 OPT_ITEM_ORDER = 28
 OPT_WAVEFRONT_SORT = 29
+OPT_CHAIN = 30
 OPT_PIXEL_FORMAT = 25
 PIXEL_ARGB = 0
 PIXEL_RGBA8 = 1

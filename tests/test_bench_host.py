@@ -71,35 +71,38 @@ def test_missing_reference_harness_is_reported_not_substituted(bench, monkeypatc
 
 
 def test_pmc_summary_used_only_for_the_same_run(bench):
-    """roofline.traffic comes from a PMC summary only when it describes this run —
-    the same image CRC and a rocprof kernel time within PMC_TIME_TOLERANCE of the live mean launch;
-    otherwise null, with the reason in roofline.pmc_refused."""
-    good = {"source": "profiles/x_pmc.json", "image_crc32": 2540294198, "mean_launch_ms_rocprof": 7.30,
-            "hbm_bytes_per_launch": 123}
-    pmc, why = bench.check_pmc(dict(good), 2540294198, 7.27, 1)
+    """roofline.traffic comes from a PMC summary only when it describes this
+    run — the same image CRC traced by the same libhippt.so (its SHA-256) — and carries bytes per
+    step, which the line divides by this run's own kernel time (a profile from a slower box no longer
+    distorts the rate); otherwise null, with the reason in roofline.pmc_refused."""
+    good = {"source": "profiles/x_pmc.json", "image_crc32": 2540294198, "lib_sha256": "ab" * 32,
+            "hbm_bytes_per_step": 123}
+    pmc, why = bench.check_pmc(dict(good), 2540294198, "ab" * 32, 1)
     assert pmc and why is None
-    pmc, why = bench.check_pmc(dict(good, image_crc32=None), 2540294198, 7.27, 1)
+    pmc, why = bench.check_pmc(dict(good, image_crc32=None), 2540294198, "ab" * 32, 1)
     assert pmc is None and "image_crc32" in why
-    pmc, why = bench.check_pmc(dict(good), 1209999578, 7.27, 1)
+    pmc, why = bench.check_pmc(dict(good), 1209999578, "ab" * 32, 1)
     assert pmc is None and "CRC" in why
-    pmc, why = bench.check_pmc(dict(good, mean_launch_ms_rocprof=8.2), 2540294198, 7.27, 1)
-    assert pmc is None and "within" in why
-    pmc, why = bench.check_pmc(dict(good), 2540294198, 7.27, 8)
+    pmc, why = bench.check_pmc(dict(good), 2540294198, "cd" * 32, 1)
+    assert pmc is None and "libhippt.so" in why
+    pmc, why = bench.check_pmc(dict(good, hbm_bytes_per_step=None), 2540294198, "ab" * 32, 1)
+    assert pmc is None and "per-step" in why
+    pmc, why = bench.check_pmc(dict(good), 2540294198, "ab" * 32, 8)
     assert pmc is None and why
-    assert bench.check_pmc(None, 1, 1.0, 1) == (None, None)
+    assert bench.check_pmc(None, 1, "x", 1) == (None, None)
 
 
 def test_pmc_candidates_first_consistent_wins(bench):
     """load_pmc returns every summary of the workload; the first consistent one is used, an older
     summary without a CRC does not hide a newer valid one."""
-    old = {"source": "profiles/round3/x_pmc.json", "image_crc32": None, "mean_launch_ms_rocprof": 18.9}
-    new = {"source": "profiles/round4/y_pmc.json", "image_crc32": 1209999578, "mean_launch_ms_rocprof": 18.88,
-           "hbm_bytes_per_launch": 7}
-    pmc, why = bench.check_pmc([old, new], 1209999578, 18.89, 1)
+    old = {"source": "profiles/round3/x_pmc.json", "image_crc32": None}
+    new = {"source": "profiles/round5/y_pmc.json", "image_crc32": 1209999578, "lib_sha256": "ef" * 32,
+           "hbm_bytes_per_step": 7}
+    pmc, why = bench.check_pmc([old, new], 1209999578, "ef" * 32, 1)
     assert pmc is new and why is None
-    pmc, why = bench.check_pmc([old], 1209999578, 18.89, 1)
+    pmc, why = bench.check_pmc([old], 1209999578, "ef" * 32, 1)
     assert pmc is None and "image_crc32" in why
-    assert bench.check_pmc([], 1, 1.0, 1) == (None, None)
+    assert bench.check_pmc([], 1, "x", 1) == (None, None)
 
 
 def test_gpus_without_launcher_starts_ranks_or_fails(bench):

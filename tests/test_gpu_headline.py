@@ -134,3 +134,39 @@ def test_config4_full_spp_rows_equal_oracle_golden(pt):
         assert pt.renderFramesAsync(spp, depth), pt.lastError()
         px, acc = pt.readback()
         check(px, acc, rows, f"share {k}/{n}")
+
+
+@pytest.mark.parametrize("name,share", [("cornell34", None), ("blob70k", None), ("cornell34", 8), ("blob70k", 8)])
+def test_bench_steps_chained_equal_oracle_golden(pt, name, share):
+    """bench.py's timed loop with chained batches (HIPPT_OPT_CHAIN 3 and 8): back-to-back async
+    steps of frames 0..63 (each step's frame 0 restarts the average), as the whole image and as a
+    1/8 interleaved row share (a SCALE rank).  The launches chain the steps, combine them beside
+    their own paths and the readback flushes the last ones; the image is still the oracle's golden
+    image (row CRCs, accumulation of the rows), and the segment and sample counts are exactly the
+    steps' sum."""
+    import hashlib
+    with open(os.path.join(GOLDEN, f"oracle_headline_{name}_1920x1080_64.json")) as f:
+        g = json.load(f)
+    pt.uploadMesh(scenes.get_scene(name))
+    if share:
+        pt.setRowInterleave(share - 1, share)
+    assert pt.initialize(g["width"], g["height"]), pt.lastError()
+    lib = hippt.load_library()
+    steps = 6 if share is None else 11
+    pt.setOption(hippt.OPT_CHAIN, 3 if share is None else 8)
+    pt.resetStats()
+    for _ in range(steps):
+        assert lib.hipptRenderFramesAsync(0, g["spp"], g["max_depth"], None)
+    px, acc = pt.readback()
+    st = pt.stats()
+    ys = range(g["height"]) if share is None else range(share - 1, g["height"], share)
+    rows = [y for y in ys if zlib.crc32(px[y].tobytes()) & 0xFFFFFFFF != g["row_crc32"][y]]
+    assert not rows, f"{len(rows)} rows differ from the oracle, first {rows[:8]}"
+    if share is None:
+        assert hashlib.sha256(acc.tobytes()).hexdigest() == g["accum_sha256"]
+        assert st["segments"] == steps * g["segments"] and st["pixelSamples"] == steps * g["pixel_samples"]
+    else:
+        assert st["pixelSamples"] == steps * len(ys) * g["width"] * g["spp"]
+    pt.setRowRange(0, 0)
+    pt.setOption(hippt.OPT_CHAIN, -1)
+

@@ -31,7 +31,7 @@ def pt():
                  (hippt.OPT_RNG_TABLE, 0), (hippt.OPT_BVH_COLLAPSE, -1), (hippt.OPT_BVH_NODE_COST, 200),
                  (hippt.OPT_BVH_LEAF4, 4), (hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_ARGB),
                  (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1), (hippt.OPT_ITEM_ORDER, -1),
-                 (hippt.OPT_WAVEFRONT_SORT, -1)):
+                 (hippt.OPT_WAVEFRONT_SORT, -1), (hippt.OPT_CHAIN, -1)):
         t.setOption(k, v)
     t.resetStats()
     yield t
@@ -638,6 +638,93 @@ def test_mesh_batches_and_frame_splits_are_bit_identical(pt):
         assert pt.renderFrames(n, 8)
     split = pt.readback()
     _assert_same(one[0], one[1], split[0], split[1])
+
+
+@pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene", "cornell_mixed"])
+def test_chained_batches_match_oracle(pt, name):
+    """HIPPT_OPT_CHAIN (Ctx::chain, hippt_trace.h chained batches): a launch whose batch is drained
+    goes on with the asynchronous batches posted behind it, the next launch combines them beside its
+    own paths, and the image's readers flush the rest.  At caps 1, 2 and 8, off and automatic, the
+    images are the oracle's: progressive batches (frames 0-1, 2-3, 4-5), batches that render the
+    same frames again (bench.py's steps: each batch's frame 0 restarts the average) more often than
+    the ring has slots, batches of different sizes (each size change a new run), a reset inside a
+    run; the pixel-sample count is exact (the chained kernels do not count samples, the host does).
+    random_scene is the general kernel over a tree in global memory, which has no camera pool and
+    never chains: its sequences run unchained under every setting."""
+    sc = scenes.get_scene(name)
+    w, h = 45, 26
+    ora6 = po.MeshScene(sc, w, h).frames(0, 6, 8)
+    ora2 = po.MeshScene(sc, w, h).frames(0, 2, 8)
+    pt.uploadMesh(sc)
+    lib = hippt.load_library()
+    for chain in (1, 2, 8, 0, -1):
+        pt.setOption(hippt.OPT_CHAIN, chain)
+        assert pt.initialize(w, h)
+        pt.resetStats()
+        for _ in range(3):
+            assert pt.renderFramesAsync(2, 8), pt.lastError()
+        got = pt.readback()
+        _assert_same(got[0], got[1], ora6[0], ora6[1])
+        assert pt.stats()["pixelSamples"] == w * h * 6
+        assert pt.initialize(w, h)
+        for _ in range(37):  # more batches than the ring's slots, and the launches' caps
+            assert lib.hipptRenderFramesAsync(0, 2, 8, None)
+        got = pt.readback()
+        _assert_same(got[0], got[1], ora2[0], ora2[1])
+        assert pt.initialize(w, h)
+        assert pt.renderFramesAsync(1, 8) and pt.renderFramesAsync(2, 8) and pt.renderFramesAsync(2, 8)
+        assert pt.renderFramesAsync(1, 8)
+        got = pt.readback()
+        _assert_same(got[0], got[1], ora6[0], ora6[1])
+        assert pt.initialize(w, h)
+        assert pt.renderFramesAsync(2, 8) and pt.renderFramesAsync(2, 8) and pt.resetAccumulation()
+        for _ in range(3):
+            assert pt.renderFramesAsync(2, 8)
+        got = pt.readback()  # (the reset restarts the frame index: frames 0..5 again)
+        _assert_same(got[0], got[1], ora6[0], ora6[1])
+
+
+def test_chained_batches_camera_change_and_row_shares(pt):
+    """A camera change between queued batches starts a new run (the old run's launches must not take
+    the new camera's batches; its combines are flushed first): the image equals one launch per batch.
+    Every 1/4 row share (hipptSetRowInterleave, bench.py's split) with chained steps renders its rows
+    of the unchained image."""
+    import ctypes
+    sc = scenes.cornell34()
+    w, h = 96, 54
+    lib = hippt.load_library()
+    moved = dict(lookfrom=(sc.lookfrom[0] + 40.0, sc.lookfrom[1] + 25.0, sc.lookfrom[2]), lookat=sc.lookat,
+                 vup=sc.vup, vfov=sc.vfov, aspect=w / h, aperture=sc.aperture, focus=sc.focus)
+    err = ctypes.c_char_p()
+    images = {}
+    for chain in (0, 8):
+        pt.setOption(hippt.OPT_CHAIN, chain)
+        pt.uploadMesh(sc)
+        assert pt.initialize(w, h)
+        for _ in range(3):
+            assert pt.renderFramesAsync(2, 8)
+        cam = hippt.build_camera(**moved)
+        assert lib.hipptSetCamera(ctypes.byref(cam), ctypes.byref(err)), err.value
+        for _ in range(3):
+            assert pt.renderFramesAsync(2, 8)
+        images[chain] = pt.readback()
+    _assert_same(images[8][0], images[8][1], images[0][0], images[0][1])
+    pt.setOption(hippt.OPT_CHAIN, 0)
+    pt.uploadMesh(sc)
+    assert pt.initialize(w, h)
+    for _ in range(4):
+        assert lib.hipptRenderFramesAsync(0, 4, 8, None)
+    full = pt.readback()
+    pt.setOption(hippt.OPT_CHAIN, 8)
+    for r in range(4):
+        pt.setRowInterleave(r, 4)
+        assert pt.initialize(w, h)
+        for _ in range(11):
+            assert lib.hipptRenderFramesAsync(0, 4, 8, None)
+        share = pt.readback()
+        rows = np.arange(r, h, 4)
+        _assert_same(share[0][rows], share[1][rows], full[0][rows], full[1][rows])
+    pt.setRowRange(0, 0)
 
 
 @pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene"])

@@ -1,9 +1,11 @@
 #!/usr/bin/env python3
 """Spill census of one kernel in a hipcc -S device assembly file: SGPR lane spills (v_writelane),
-their reloads (v_readlane), VGPR scratch spills/reloads, and the static instruction count.
+their reloads (v_readlane), VGPR scratch spills/reloads (with the loop depth of the block each sits
+in, from LLVM's '; in Loop: ... Depth=N' block comments) and the static instruction count.
 usage: tools/kspill.py build_hippt_kernels.s PATTERN [PATTERN ...]  (substring of the mangled name)"""
 import re
 import sys
+from collections import Counter
 
 text = open(sys.argv[1]).read().split("\n")
 starts = [(i, l.split(":")[0]) for i, l in enumerate(text) if re.match(r"^_Z\S+:", l)]
@@ -14,8 +16,17 @@ for pat in sys.argv[2:]:
         j = i
         while not text[j].strip().startswith(".Lfunc_end"):
             j += 1
-        body = [l.strip() for l in text[i:j]]
-        ins = [l for l in body if l and not l.startswith((".", ";")) and not l.endswith(":")]
-        c = lambda p: sum(1 for l in ins if l.startswith(p))
-        print(f"{name[-60:]}: {len(ins)} instr, writelane {c('v_writelane')}, readlane {c('v_readlane')}, "
-              f"scratch_store {c('scratch_store')}, scratch_load {c('scratch_load')}, v_ {c('v_')}, s_ {c('s_')}")
+        depth = 0
+        ins = []
+        for l in text[i:j]:
+            s = l.strip()
+            m = re.search(r"Depth=(\d+)", s)
+            if re.match(r"^(\.LBB|; %bb)", s):
+                depth = int(m.group(1)) if m else 0
+                continue
+            if s and not s.startswith((".", ";")) and not s.endswith(":"):
+                ins.append((s, depth))
+        c = lambda p: sum(1 for s, _ in ins if s.startswith(p))
+        sd = Counter(d for s, d in ins if s.startswith("scratch_"))
+        print(f"{name[-48:]}: {len(ins)} instr, writelane {c('v_writelane')}, readlane {c('v_readlane')}, "
+              f"scratch {c('scratch_store')}st/{c('scratch_load')}ld by loop depth {dict(sorted(sd.items()))}")

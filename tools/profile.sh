@@ -1,7 +1,7 @@
 #!/bin/bash
 # tools/profile.sh TAG [bench args...] — run ON THE GPU BOX (via gpurun).
 #
-# 1. rocprofv3 --kernel-trace --stats over a short bench run  -> gpurun_out/prof_TAG/kt
+# 1. rocprofv3 --kernel-trace --stats over the driver's bench run (20 steps after 5) -> gpurun_out/prof_TAG/kt
 # 2. separate --pmc passes (FETCH_SIZE; WRITE_SIZE; SQ counters) -> gpurun_out/prof_TAG/pmc*
 #    (one TCC counter group per pass: FETCH_SIZE and WRITE_SIZE do not fit together)
 # Every step has its own time limit and the chain stops at the first failure.
@@ -13,7 +13,8 @@ export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 OUT=gpurun_out/prof_${TAG}
 mkdir -p "$OUT"
-ARGS=(--steps 3 --warmup 1 --cpu-baseline off "$@")
+ARGS=(--steps 20 --warmup 5 --cpu-baseline off "$@")
+sha256sum qt-raytracer_amd/libhippt.so > "$OUT/lib.sha256"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -T --output-format csv -d "$OUT/kt" -o run -- \
     python3 bench.py "${ARGS[@]}" > "$OUT/kt_bench.json" 2> "$OUT/kt_bench.err"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -T --output-format csv -d "$OUT/pmc_fetch" -o run -- \
