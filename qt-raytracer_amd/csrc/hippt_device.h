@@ -134,15 +134,15 @@ struct MeshParams {
 // the first batch not yet combined after the launches of epoch parity 0 / 1 (+0 / +32), the combine
 // chunk counters of epoch parity 0 / 1 (+64 / +96).
 constexpr unsigned kChainSlotsMax = 16, kChainBlockWords = 8 * 32 + 32, kChainMarkerWord = 8 * 32;
-constexpr unsigned kChainCtlWord = kChainSlotsMax * kChainBlockWords, kChainCtlWords = kChainCtlWord + 224;
-// (+128: a device copy of the host mailbox word, 64-bit; +160: the realtime stamp of its last
-// completed refresh; +192: the stamp of the last claimed refresh)
-constexpr unsigned kChainBoxCacheWord = kChainCtlWord + 128, kChainBoxStampWord = kChainCtlWord + 160,
-                   kChainBoxClaimWord = kChainCtlWord + 192;
+constexpr unsigned kChainCtlWord = kChainSlotsMax * kChainBlockWords;
+// (+128: kQueues device copies of the host mailbox, one 128-byte line each, for the blocks of one
+// XCD: the copy (64-bit), the realtime stamp of its last completed refresh, the stamp of the last
+// claimed refresh)
+constexpr unsigned kChainBoxWord = kChainCtlWord + 128, kChainCtlWords = kChainBoxWord + 8 * 32;
 // batches of at most 2^kChainMaxShift items chain (the slot bits above them, kNone above all)
 constexpr unsigned kChainMaxShift = 27;
 // camera-pool kernels: per-wave state words in LDS before each wave's pool (trace::WaveWords)
-constexpr unsigned kWaveWords = 16;
+constexpr unsigned kWaveWords = 20;
 
 // The chain's final combine (launch_chain_flush): every batch of the run that no launch combined,
 // [first uncombined (from the control block, launch epoch `epoch`), lastSeq], in order per pixel.

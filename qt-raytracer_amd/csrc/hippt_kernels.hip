@@ -421,13 +421,15 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     unsigned poolNext = 64;
     WaveWords *const ww = reinterpret_cast<WaveWords *>(pool - kWW);
     ChainWave *const cw = &ww->cw;
+    ChainView *const view = &reinterpret_cast<WaveWords *>(reinterpret_cast<char *>(lds) + P.poolOffset)->view;
     // CHAIN kernels keep the work queue and the segment count in LDS (ww->Q, ww->segs), the others in
     // registers
     WorkQueue Q;
     if constexpr (CHAIN) {
-        chain_begin(Q, cw);
+        chain_begin(Q, cw, view);
         store_queue(&ww->Q, Q);
         if (__lane_id() == 0) ww->segs = 0;
+        __syncthreads();  // the block's mailbox view (its first wave's) is initialised
     } else {
         queue_begin(Q, P.totalItems, P.chunk);
     }
@@ -539,7 +541,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                                 tItem = t;
                                 want = false;
                             }
-                            if (!__ballot(want) || !chain_next(Q, cw)) break;
+                            if (!__ballot(want) || !chain_next(Q, cw, view)) break;
                         }
                         store_queue(&ww->Q, Q);
                         it = order_item_late(raw);
@@ -696,13 +698,6 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         }
     }
     while (combLeft) combLeft = comb_step();
-    if (CHAIN && __lane_id() == 0) {
-        // for the next launch: the first batch not combined after this one (ChainWave::c0..c1 done)
-        const int c0 = int(cw->c0), c1 = int(cw->c1);
-        unsigned *const ctl = late_field(chainCtl);
-        __hip_atomic_store(ctl + kChainCtlWord + 32u * (late_field(chainEpoch) & 1u), unsigned(max(c0, c1 + 1)),
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
 #ifdef HIPPT_DEBUG_RATE
     rt_flush(0);
 #endif
@@ -748,8 +743,7 @@ __global__ __launch_bounds__(256) void combine_kernel(CombineParams P, HostFrame
 
 // The chain's final combine (ChainFlushParams): every batch of the run no launch combined, in order.
 __global__ __launch_bounds__(256) void chain_flush_kernel(ChainFlushParams P) {
-    const int c0 = int(__hip_atomic_load(P.ctl + kChainCtlWord + 32u * ((P.epoch + 1u) & 1u), __ATOMIC_RELAXED,
-                                         __HIP_MEMORY_SCOPE_AGENT));
+    const int c0 = int(P.ctl[kChainCtlWord + 32u * ((P.epoch + 1u) & 1u)]);  // (written by an earlier launch)
     const int c1 = int(P.lastSeq);
     if (c1 < c0) return;
     const unsigned stride = gridDim.x * 256u;

@@ -355,6 +355,20 @@ struct ChainWave {
     unsigned c0, c1;    // this launch's combine range (c1 < c0: none)
     unsigned stat;      // the batch whose queues have static first chunks (~0u: none)
 };
+
+// The block's view of the mailbox (in its first wave's WaveWords; chain_next): batches before
+// `posted` are posted (frames `step` apart), and the last refresh of the view was at `stamp` (low
+// 32 bits of the 100 MHz clock), so that a block's waves reaching their batch's end within
+// kViewRefresh of each other ask the device-wide copy once.
+struct ChainView {
+    unsigned posted;
+    int step;
+    unsigned stamp;
+    unsigned spare;
+};
+
+#define late_field(f) late_arg_at<decltype(MeshParams::f)>(unsigned(offsetof(MeshParams, f)))
+
 // The camera-pool kernels' per-wave state kept in LDS between uses, kWaveWords words at the start of
 // each wave's pool block: the work queue (read and written back at each pool refill, once per 64
 // items), the wave's segment count and the chain state.  In registers they would be live across the
@@ -364,6 +378,7 @@ struct WaveWords {
     WorkQueue Q;
     unsigned segs;
     ChainWave cw;
+    ChainView view;  // (the block's first wave's only)
 };
 static_assert(sizeof(WaveWords) == kWaveWords * 4, "per-wave LDS words");
 
@@ -382,17 +397,20 @@ __device__ __forceinline__ void store_queue(WorkQueue *q, const WorkQueue &Q) {
     if (__lane_id() == 0) *q = Q;
 }
 
-#define late_field(f) late_arg_at<decltype(MeshParams::f)>(unsigned(offsetof(MeshParams, f)))
-
 __device__ __forceinline__ unsigned *chain_block(unsigned *ctl, unsigned t, unsigned slots) {
     return ctl + (t & (slots - 1u)) * kChainBlockWords;
 }
 
+// Cross-launch words (markers, the combined-through word, counter resets) are plain loads and stores:
+// a launch reads only what earlier launches wrote (the kernel boundary writes the L2s back and
+// invalidates them), and every wave of a launch writes the same value.  Uncached (agent-scope) loads
+// of one line by every wave of a launch serialise at the memory side: ~0.3 ms per launch (r5g).
+
 // Batch t taken by launch `epoch` (lane 0; every wave that moves into t stores the same word).
 __device__ __forceinline__ void chain_mark(unsigned *ctl, unsigned t, unsigned slots, unsigned epoch) {
     if (__lane_id() == 0)
-        __hip_atomic_store(reinterpret_cast<unsigned long long *>(chain_block(ctl, t, slots) + kChainMarkerWord),
-                           ((unsigned long long)t << 32) | (epoch + 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *reinterpret_cast<unsigned long long *>(chain_block(ctl, t, slots) + kChainMarkerWord) =
+            ((unsigned long long)t << 32) | (epoch + 1u);
 }
 
 // queue_select for a batch with (stat) or without static first chunks
@@ -402,23 +420,21 @@ __device__ __forceinline__ void chain_select(WorkQueue &Q, unsigned g, unsigned 
 }
 
 // Kernel start of a CHAIN launch (whole wave): the combine range, the first batch to trace and the
-// wave's queue (static first chunk when that batch is the launch's own), state into *cw.
-__device__ __forceinline__ void chain_begin(WorkQueue &Q, ChainWave *cw) {
+// wave's queue (static first chunk when that batch is the launch's own), state into *cw; the block's
+// first wave also initialises the block's mailbox view.
+__device__ __forceinline__ void chain_begin(WorkQueue &Q, ChainWave *cw, ChainView *view) {
     unsigned *const ctl = late_field(chainCtl);
     const unsigned e = late_field(chainEpoch), own = late_field(chainSeq), R = late_field(chainSlots);
     const unsigned total = late_field(totalItems), chunk = late_field(chunk);
-    unsigned c0 = 0;
-    if (__lane_id() == 0)
-        c0 = __hip_atomic_load(ctl + kChainCtlWord + 32u * ((e + 1u) & 1u), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    c0 = __builtin_amdgcn_readfirstlane(c0);
+    // the first batch not combined by an earlier launch (written at the previous launch's start)
+    const unsigned c0 = __builtin_amdgcn_readfirstlane(ctl[kChainCtlWord + 32u * ((e + 1u) & 1u)]);
     // lane k: batch t0 + k finished by an earlier launch (its slot's marker), within the ring's window
     const unsigned t0 = max(own, c0);
     bool fin = false;
     if (__lane_id() < R && t0 + __lane_id() < c0 + R) {
         const unsigned t = t0 + __lane_id();
-        const unsigned long long m = __hip_atomic_load(
-            reinterpret_cast<const unsigned long long *>(chain_block(ctl, t, R) + kChainMarkerWord), __ATOMIC_RELAXED,
-            __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned long long m =
+            *reinterpret_cast<const unsigned long long *>(chain_block(ctl, t, R) + kChainMarkerWord);
         const unsigned by = unsigned(m);
         fin = unsigned(m >> 32) == t && by != 0u && by <= e;
     }
@@ -436,67 +452,97 @@ __device__ __forceinline__ void chain_begin(WorkQueue &Q, ChainWave *cw) {
         cw->step = step;
         cw->t = u == own ? own : u - 1u;
         cw->stat = u == own ? own : ~0u;
+        if (threadIdx.x == 0) {
+            view->posted = own + 1u;
+            view->step = step;
+            view->stamp = 0;
+        }
     }
     if (u == own) {  // the own batch, untaken: first chunks static, as unchained
         chain_mark(ctl, own, R, e);
         queue_begin(Q, total, chunk);
-    } else {  // nothing to fetch: the wave's first loop ends at once and chain_next moves into batch u
+    } else {  // nothing to fetch: the wave's first refill moves it into batch u (chain_next)
         Q.left = 0;
         Q.next = Q.end = 0;
     }
-    // this launch's bookkeeping for the next: block 0's first wave zeroes the next epoch's combine
-    // counter and the work counters of the slots combined here (their next batches' counters)
+    // this launch's bookkeeping for the next (block 0's first wave): the first batch not combined
+    // after this launch (its combines are done by its end), the next epoch's combine counter, and
+    // the work counters of the slots combined here (the counters of their next batches)
     if (blockIdx.x == 0 && threadIdx.x < 64u) {
-        if (__lane_id() == 0)
-            __hip_atomic_store(ctl + kChainCtlWord + 64u + 32u * ((e + 1u) & 1u), 0u, __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+        if (__lane_id() == 0) {
+            ctl[kChainCtlWord + 32u * (e & 1u)] = unsigned(max(int(c0), c1 + 1));
+            ctl[kChainCtlWord + 64u + 32u * ((e + 1u) & 1u)] = 0u;
+        }
         for (int b = int(c0); b <= c1; ++b)
-            if (__lane_id() < kQueues)
-                __hip_atomic_store(chain_block(ctl, unsigned(b), R) + __lane_id() * kQueueStride, 0u, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+            if (__lane_id() < kQueues) chain_block(ctl, unsigned(b), R)[__lane_id() * kQueueStride] = 0u;
     }
 }
 
 // A wave whose batch is drained moves into the next batch of the run, if this launch may take it and
 // the mailbox shows it posted (whole wave; at a camera-pool refill, so that the lanes whose paths
 // ended take the next batch's items while the others go on with theirs).
-__device__ __forceinline__ bool chain_next(WorkQueue &Q, ChainWave *cw) {
+__device__ __forceinline__ bool chain_next(WorkQueue &Q, ChainWave *cw, ChainView *view) {
     const unsigned nt = __builtin_amdgcn_readfirstlane(cw->t) + 1u;
     if (nt > __builtin_amdgcn_readfirstlane(cw->tLim)) return false;
     int step = int(__builtin_amdgcn_readfirstlane(unsigned(cw->step)));
     if (nt >= __builtin_amdgcn_readfirstlane(cw->posted)) {
-        // one 64-bit mailbox word: run << 33 | consecutive frames << 32 | last posted batch.  The host
-        // word is read over PCIe, and such reads serialise (~60 ns each: 7168 waves reaching their
-        // batch's end together waited 0.43 ms, r5d/r5e).  A device copy serves the launch's waves: a
-        // wave whose copy is not current refreshes it from the host only if the last refresh is older
-        // than kBoxRefresh ticks of the 100 MHz clock and it wins the refresh claim; a wave that loses
-        // the claim waits (bounded) for the winner's refresh to land.
-        constexpr unsigned long long kBoxRefresh = 1000;  // 10 us
+        // The mailbox (one 64-bit word: run << 33 | consecutive frames << 32 | last posted batch) is
+        // host memory read over PCIe, and such reads serialise (~60 ns each: 7168 waves reaching their
+        // batch's end together waited 0.43-1.1 ms, r5d/r5e).  Three levels: the block's view in LDS
+        // (ChainView), a per-XCD device copy refreshed from the host by one claiming wave at most
+        // every kBoxRefresh, and the host word.
+        constexpr unsigned long long kBoxRefresh = 1000;  // 10 us of the 100 MHz clock
+        constexpr unsigned kViewRefresh = 500;
         unsigned lo = 0, hi = 0;
+        bool known = false;
         if (__lane_id() == 0) {
-            unsigned *const ctl0 = late_field(chainCtl);
-            auto *cache = reinterpret_cast<unsigned long long *>(ctl0 + kChainBoxCacheWord);
-            auto *stamp = reinterpret_cast<unsigned long long *>(ctl0 + kChainBoxStampWord);
-            auto *claim = reinterpret_cast<unsigned long long *>(ctl0 + kChainBoxClaimWord);
-            unsigned long long b = __hip_atomic_load(cache, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned run = late_field(chainRun);
-            const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-            if (!(unsigned(b >> 33) == run && unsigned(b) >= nt) &&
-                now - __hip_atomic_load(stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= kBoxRefresh) {
-                const unsigned long long prev = atomicExch(claim, now);
-                if (now - prev >= kBoxRefresh) {  // this wave refreshes the copy
-                    b = __hip_atomic_load(late_field(chainBox), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                    atomicMax(cache, b);  // (a run's words grow: run in the high bits, then the batch)
-                    __hip_atomic_store(stamp, now, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                } else {  // another wave's refresh (claimed at `prev`) is in flight
-                    for (unsigned k = 0; k < 4096u && __hip_atomic_load(stamp, __ATOMIC_ACQUIRE,
-                                                                         __HIP_MEMORY_SCOPE_AGENT) < prev; ++k)
-                        __builtin_amdgcn_s_sleep(2);
-                    b = __hip_atomic_load(cache, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                }
+            const unsigned vp = view->posted, now32 = unsigned(__builtin_amdgcn_s_memrealtime());
+            if (nt < vp) {  // the block already knows it posted
+                known = true;
+                lo = vp - 1u;
+                hi = (late_field(chainRun) << 1) | (view->step > 0 ? 1u : 0u);
+            } else if (view->stamp != 0u && now32 - view->stamp < kViewRefresh) {
+                known = true;  // the block asked moments ago: not posted
+                lo = vp - 1u;
+                hi = late_field(chainRun) << 1;
             }
-            lo = unsigned(b);
-            hi = unsigned(b >> 32);
+        }
+        if (!__builtin_amdgcn_readfirstlane(unsigned(known))) {
+            if (__lane_id() == 0) {
+                // this XCD's copy (blocks b = XCD mod 8): uncached loads of one line serialise at the
+                // memory side, ~20 ns each, so the device's 1792 blocks share 8 lines, not one
+                auto *box = reinterpret_cast<unsigned long long *>(late_field(chainCtl) + kChainBoxWord +
+                                                                    (blockIdx.x % kQueues) * 32u);
+                unsigned long long *const cache = box, *const stamp = box + 1, *const claim = box + 2;
+                unsigned long long b = __hip_atomic_load(cache, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                const unsigned run = late_field(chainRun);
+                const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+                if (!(unsigned(b >> 33) == run && unsigned(b) >= nt) &&
+                    now - __hip_atomic_load(stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= kBoxRefresh) {
+                    // the claim: a compare-and-swap from a stale claim stamp (a losing wave does not
+                    // move the claim, so the stamp it waits for is the winner's)
+                    unsigned long long prev = __hip_atomic_load(claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const bool mine = now - prev >= kBoxRefresh && atomicCAS(claim, prev, now) == prev;
+                    if (mine) {  // this wave refreshes the copy
+                        b = __hip_atomic_load(late_field(chainBox), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                        atomicMax(cache, b);  // (a run's words grow: run in the high bits, then the batch)
+                        __hip_atomic_store(stamp, now, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+                    } else {  // another wave's refresh is in flight: wait for it, 50 us at most
+                        prev = __hip_atomic_load(claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        while (__hip_atomic_load(stamp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < prev &&
+                               __builtin_amdgcn_s_memrealtime() - now < 5 * kBoxRefresh)
+                            __builtin_amdgcn_s_sleep(4);
+                        b = __hip_atomic_load(cache, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+                lo = unsigned(b);
+                hi = unsigned(b >> 32);
+                if ((hi >> 1) == run) {  // into the block's view
+                    atomicMax(&view->posted, lo + 1u);
+                    view->step = (hi & 1u) ? late_field(frames) : 0;
+                }
+                view->stamp = max(unsigned(__builtin_amdgcn_s_memrealtime()), 1u);
+            }
         }
         lo = __builtin_amdgcn_readfirstlane(lo);
         hi = __builtin_amdgcn_readfirstlane(hi);
