@@ -637,10 +637,12 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         // ---- shading: lanes whose traversal finished (ray_color step, RayTracer.h:579-596) ----
         // (a lane resuming a pending draw continues its segment; CHAIN kernels count the wave's
         // segments in ww->segs, one LDS add per round)
+#ifndef HIPPT_EXP_CHAIN_NOSEGS
         if constexpr (CHAIN) {
             const unsigned long long sm = __ballot(item != kNone && !busy(T) && !(CAP && pend != 0u));
             if (__lane_id() == 0 && sm) atomicAdd(&ww->segs, unsigned(__popcll(sm)));
         }
+#endif
         if (item != kNone && !busy(T)) {
             prof<STATS>(pc, 6);
             const bool cont = CAP && pend != 0u;  // resumes a pending draw: same segment

@@ -356,15 +356,15 @@ struct ChainWave {
     unsigned stat;      // the batch whose queues have static first chunks (~0u: none)
 };
 
-// The block's view of the mailbox (in its first wave's WaveWords; chain_next): batches before
-// `posted` are posted (frames `step` apart), and the last refresh of the view was at `stamp` (low
-// 32 bits of the 100 MHz clock), so that a block's waves reaching their batch's end within
-// kViewRefresh of each other ask the device-wide copy once.
+// The block's view of the mailbox (in its first wave's WaveWords; chain_next): batches up to `last`
+// are posted (frames apart when `consec`; none after them when `closed`: the host is on a later run),
+// as learnt at `stamp` (low 32 bits of the 100 MHz clock) by the block's querier; `busy` while one
+// wave asks the device copy for the block, so that the block's other waves wait in LDS.
 struct ChainView {
-    unsigned posted;
-    int step;
+    unsigned last;
+    unsigned flags;  // bit 0: consecutive frames; bit 1: closed
     unsigned stamp;
-    unsigned spare;
+    unsigned busy;
 };
 
 #define late_field(f) late_arg_at<decltype(MeshParams::f)>(unsigned(offsetof(MeshParams, f)))
@@ -453,9 +453,10 @@ __device__ __forceinline__ void chain_begin(WorkQueue &Q, ChainWave *cw, ChainVi
         cw->t = u == own ? own : u - 1u;
         cw->stat = u == own ? own : ~0u;
         if (threadIdx.x == 0) {
-            view->posted = own + 1u;
-            view->step = step;
+            view->last = own;
+            view->flags = step > 0 ? 1u : 0u;
             view->stamp = 0;
+            view->busy = 0;
         }
     }
     if (u == own) {  // the own batch, untaken: first chunks static, as unchained
@@ -478,6 +479,73 @@ __device__ __forceinline__ void chain_begin(WorkQueue &Q, ChainWave *cw, ChainVi
     }
 }
 
+// Is batch nt posted?  (lane 0 of a wave; out: the last batch known posted and the view's flags.)
+// The mailbox (one 64-bit word: run << 33 | consecutive frames << 32 | last posted batch) is host
+// memory read over PCIe, where reads serialise (~60 ns each: 7168 waves reaching their batch's end
+// together waited 0.43-1.1 ms, r5d/r5e), and uncached loads of one device line serialise too (~20 ns:
+// every wave asking a device-wide copy cost ~130 us per launch, r5i).  So three levels, each asked
+// by one wave for many: the block's view in LDS (one querier per block, the others wait in LDS), a
+// per-XCD device copy (one 64-bit word: its refresh stamp, closed, consecutive, last batch) that a
+// querier finding it older than kBoxRefresh refreshes from the host after winning a claim, and the
+// host word.  A querier that loses the claim sleeps (no memory traffic) for the winner's refresh,
+// then reads the copy once more.  Stale answers only ever say "not yet posted": a wave then stops
+// taking batches, and a later launch traces them.
+__device__ __forceinline__ void chain_copy_pack(unsigned long long now, unsigned long long h, unsigned run,
+                                                unsigned long long &c) {
+    // the host on a later run: this one is closed (and the word's batch is that run's)
+    const bool closed = unsigned(h >> 33) != run;
+    c = ((now >> 4) << 40) | (closed ? (1ull << 33) : (h & ((1ull << 33) - 1ull)));
+}
+__device__ __forceinline__ void chain_ask(unsigned nt, ChainView *view, unsigned &last, unsigned &flags) {
+    constexpr unsigned long long kBoxRefresh = 1000;  // 10 us of the 100 MHz clock
+    constexpr unsigned kViewRefresh = 500, kWaitBusy = 20000;
+    const unsigned t0 = unsigned(__builtin_amdgcn_s_memrealtime());
+    for (;;) {
+        last = __hip_atomic_load(&view->last, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        flags = __hip_atomic_load(&view->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const unsigned st = __hip_atomic_load(&view->stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const unsigned now32 = unsigned(__builtin_amdgcn_s_memrealtime());
+        if (nt <= last || (flags & 2u) || (st != 0u && now32 - st < kViewRefresh)) return;
+        unsigned idle = 0u;
+        if (__hip_atomic_compare_exchange_strong(&view->busy, &idle, 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
+                                                 __HIP_MEMORY_SCOPE_WORKGROUP))
+            break;  // this wave asks for the block
+        // another wave of the block is asking: wait for its answer (bounded), then take the view
+        while (__hip_atomic_load(&view->busy, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP) != 0u &&
+               unsigned(__builtin_amdgcn_s_memrealtime()) - t0 < kWaitBusy)
+            __builtin_amdgcn_s_sleep(2);
+        last = __hip_atomic_load(&view->last, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        flags = __hip_atomic_load(&view->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        return;
+    }
+    unsigned long long *const box = reinterpret_cast<unsigned long long *>(late_field(chainCtl) + kChainBoxWord +
+                                                                          (blockIdx.x % kQueues) * 32u);
+    unsigned long long *const copy = box, *const claim = box + 1;
+    const unsigned run = late_field(chainRun);
+    const unsigned long long now = __builtin_amdgcn_s_memrealtime();
+    unsigned long long c = __hip_atomic_load(copy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned age = (unsigned(now >> 4) - unsigned(c >> 40)) & 0xffffffu;  // in 16-tick units
+    if (unsigned(c) < nt && !((c >> 33) & 1ull) && age >= kBoxRefresh / 16u) {
+        unsigned long long prev = __hip_atomic_load(claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (now - prev >= kBoxRefresh && atomicCAS(claim, prev, now) == prev) {  // this wave refreshes
+            const unsigned long long h =
+                __hip_atomic_load(late_field(chainBox), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+            chain_copy_pack(__builtin_amdgcn_s_memrealtime(), h, run, c);
+            __hip_atomic_store(copy, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {  // a refresh is in flight (claimed at most kBoxRefresh ago): give it 4 us, read once more
+            while (__builtin_amdgcn_s_memrealtime() - now < 400u) __builtin_amdgcn_s_sleep(8);
+            c = __hip_atomic_load(copy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
+    last = max(last, unsigned(c));
+    flags = unsigned(c >> 32) & 3u;
+    __hip_atomic_store(&view->flags, flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(&view->last, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(&view->stamp, max(unsigned(__builtin_amdgcn_s_memrealtime()), 1u), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_WORKGROUP);
+    __hip_atomic_store(&view->busy, 0u, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
 // A wave whose batch is drained moves into the next batch of the run, if this launch may take it and
 // the mailbox shows it posted (whole wave; at a camera-pool refill, so that the lanes whose paths
 // ended take the next batch's items while the others go on with theirs).
@@ -486,70 +554,14 @@ __device__ __forceinline__ bool chain_next(WorkQueue &Q, ChainWave *cw, ChainVie
     if (nt > __builtin_amdgcn_readfirstlane(cw->tLim)) return false;
     int step = int(__builtin_amdgcn_readfirstlane(unsigned(cw->step)));
     if (nt >= __builtin_amdgcn_readfirstlane(cw->posted)) {
-        // The mailbox (one 64-bit word: run << 33 | consecutive frames << 32 | last posted batch) is
-        // host memory read over PCIe, and such reads serialise (~60 ns each: 7168 waves reaching their
-        // batch's end together waited 0.43-1.1 ms, r5d/r5e).  Three levels: the block's view in LDS
-        // (ChainView), a per-XCD device copy refreshed from the host by one claiming wave at most
-        // every kBoxRefresh, and the host word.
-        constexpr unsigned long long kBoxRefresh = 1000;  // 10 us of the 100 MHz clock
-        constexpr unsigned kViewRefresh = 500;
-        unsigned lo = 0, hi = 0;
-        bool known = false;
+        unsigned last = 0, flags = 0;
+        if (__lane_id() == 0) chain_ask(nt, view, last, flags);
+        last = __builtin_amdgcn_readfirstlane(last);
+        flags = __builtin_amdgcn_readfirstlane(flags);
+        if (nt > last) return false;  // not (yet) posted, or the run is closed
+        step = (flags & 1u) ? late_field(frames) : 0;
         if (__lane_id() == 0) {
-            const unsigned vp = view->posted, now32 = unsigned(__builtin_amdgcn_s_memrealtime());
-            if (nt < vp) {  // the block already knows it posted
-                known = true;
-                lo = vp - 1u;
-                hi = (late_field(chainRun) << 1) | (view->step > 0 ? 1u : 0u);
-            } else if (view->stamp != 0u && now32 - view->stamp < kViewRefresh) {
-                known = true;  // the block asked moments ago: not posted
-                lo = vp - 1u;
-                hi = late_field(chainRun) << 1;
-            }
-        }
-        if (!__builtin_amdgcn_readfirstlane(unsigned(known))) {
-            if (__lane_id() == 0) {
-                // this XCD's copy (blocks b = XCD mod 8): uncached loads of one line serialise at the
-                // memory side, ~20 ns each, so the device's 1792 blocks share 8 lines, not one
-                auto *box = reinterpret_cast<unsigned long long *>(late_field(chainCtl) + kChainBoxWord +
-                                                                    (blockIdx.x % kQueues) * 32u);
-                unsigned long long *const cache = box, *const stamp = box + 1, *const claim = box + 2;
-                unsigned long long b = __hip_atomic_load(cache, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                const unsigned run = late_field(chainRun);
-                const unsigned long long now = __builtin_amdgcn_s_memrealtime();
-                if (!(unsigned(b >> 33) == run && unsigned(b) >= nt) &&
-                    now - __hip_atomic_load(stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) >= kBoxRefresh) {
-                    // the claim: a compare-and-swap from a stale claim stamp (a losing wave does not
-                    // move the claim, so the stamp it waits for is the winner's)
-                    unsigned long long prev = __hip_atomic_load(claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const bool mine = now - prev >= kBoxRefresh && atomicCAS(claim, prev, now) == prev;
-                    if (mine) {  // this wave refreshes the copy
-                        b = __hip_atomic_load(late_field(chainBox), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-                        atomicMax(cache, b);  // (a run's words grow: run in the high bits, then the batch)
-                        __hip_atomic_store(stamp, now, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
-                    } else {  // another wave's refresh is in flight: wait for it, 50 us at most
-                        prev = __hip_atomic_load(claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        while (__hip_atomic_load(stamp, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) < prev &&
-                               __builtin_amdgcn_s_memrealtime() - now < 5 * kBoxRefresh)
-                            __builtin_amdgcn_s_sleep(4);
-                        b = __hip_atomic_load(cache, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    }
-                }
-                lo = unsigned(b);
-                hi = unsigned(b >> 32);
-                if ((hi >> 1) == run) {  // into the block's view
-                    atomicMax(&view->posted, lo + 1u);
-                    view->step = (hi & 1u) ? late_field(frames) : 0;
-                }
-                view->stamp = max(unsigned(__builtin_amdgcn_s_memrealtime()), 1u);
-            }
-        }
-        lo = __builtin_amdgcn_readfirstlane(lo);
-        hi = __builtin_amdgcn_readfirstlane(hi);
-        if ((hi >> 1) != late_field(chainRun) || nt > lo) return false;  // not (yet) posted, or a later run
-        step = (hi & 1u) ? late_field(frames) : 0;
-        if (__lane_id() == 0) {
-            cw->posted = lo + 1u;
+            cw->posted = last + 1u;
             cw->step = step;
         }
     }

@@ -101,6 +101,11 @@ def main():
             c.update(vals)
     cfg = bench["config"]
     f_fetch, f_write, model = traffic_model(cfg["scene"])
+    try:
+        with open(FACTORS) as f:
+            cal = {k: {m: v[m] for m in ("fetch_factor", "write_factor") if m in v} for k, v in json.load(f).items()}
+    except OSError:
+        cal = None
     fetch_raw = c.get("FETCH_SIZE", 0.0) * 1024
     write_raw = c.get("WRITE_SIZE", 0.0) * 1024
     hbm = f_fetch * fetch_raw + f_write * write_raw
@@ -122,6 +127,8 @@ def main():
         "hbm_bytes_per_step": int(hbm), "fetch_bytes_raw_per_step": int(fetch_raw),
         "write_bytes_raw_per_step": int(write_raw), "write_bytes_per_step": int(write),
         "traffic_model": model,
+        # per access width: bytes moved / counter bytes, measured on known byte counts (pmc_bytes.hip)
+        "pmc_factors": cal,
         "alg_bytes_per_step": bench["roofline"]["algorithmic_bytes"].get("per_step"),
         "flop_per_step": bench["roofline"].get("flop_per_step"),
         "lib_sha256": lib_sha,

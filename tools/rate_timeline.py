@@ -4,7 +4,8 @@ HIPPT_LIB=qt-raytracer_amd/libv_rate.so): samples and segments finished per 10 u
 rounds and lane occupancy, for a list of (stride, spp) jobs, so that a 1/N row share can be compared
 with the whole image bucket by bucket.
 
-usage: python tools/rate_timeline.py [--scene cornell34] [--jobs 1:64,8:64,1:8] [--bucket-us 50]
+usage: python tools/rate_timeline.py [--scene cornell34] [--jobs 1:64,8:64,1:8,8:64:8] [--bucket-us 50]
+       (a job is stride:spp[:batches]; batches > 1 are submitted back to back before one sync)
        [KEY=VALUE option pairs]
 """
 import argparse
@@ -23,7 +24,7 @@ from hippt import scenes  # noqa: E402
 NB = 1024
 
 
-def run(scene, stride, spp, opts, agg):
+def run(scene, stride, spp, opts, agg, batches=1):
     pt = hippt.PathTracer()
     pt.setDevices([0])
     for k, v in opts:
@@ -40,7 +41,8 @@ def run(scene, stride, spp, opts, agg):
     buf = np.zeros((NB, 5), np.uint64)
     fn(None, 1)
     pt.resetStats()
-    pt._lib.hipptRenderFramesAsync(0, spp, 8, None)
+    for b in range(batches):  # back-to-back async batches (chained with HIPPT_OPT_CHAIN)
+        pt._lib.hipptRenderFramesAsync(b * spp, spp, 8, None)
     pt.synchronize()
     st = pt.stats()
     fn(buf.ctypes.data, 1)
@@ -59,7 +61,7 @@ def run(scene, stride, spp, opts, agg):
                      "segs_per_us": round(b[i, 1] / agg / 1e3, 2),  # G segments/s
                      "lane_util": round(b[i, 3] / max(1, 64 * b[i, 2]), 3),
                      "waves": round(b[i, 4] / k, 0)})
-    return {"scene": scene, "stride": stride, "spp": spp, "trace_ms": round(st["traceMs"], 4),
+    return {"scene": scene, "stride": stride, "spp": spp, "batches": batches, "trace_ms": round(st["traceMs"], 4),
             "segments": int(st["segments"]), "samples": int(st["pixelSamples"]),
             "gseg_per_s": round(st["segments"] / st["traceMs"] / 1e6, 2), "buckets": rows}
 
@@ -73,8 +75,8 @@ def main():
     a = ap.parse_args()
     opts = [tuple(int(x) for x in o.split("=")) for o in a.opts]
     for j in a.jobs.split(","):
-        stride, spp = (int(x) for x in j.split(":"))
-        print(json.dumps(run(a.scene, stride, spp, opts, a.bucket_us)), flush=True)
+        f = [int(x) for x in j.split(":")]
+        print(json.dumps(run(a.scene, f[0], f[1], opts, a.bucket_us, f[2] if len(f) > 2 else 1)), flush=True)
 
 
 if __name__ == "__main__":
