@@ -142,7 +142,7 @@ constexpr unsigned kChainBoxWord = kChainCtlWord + 128, kChainCtlWords = kChainB
 // batches of at most 2^kChainMaxShift items chain (the slot bits above them, kNone above all)
 constexpr unsigned kChainMaxShift = 27;
 // camera-pool kernels: per-wave state words in LDS before each wave's pool (trace::WaveWords)
-constexpr unsigned kWaveWords = 20;
+constexpr unsigned kWaveWords = 22;
 
 // The chain's final combine (launch_chain_flush): every batch of the run that no launch combined,
 // [first uncombined (from the control block, launch epoch `epoch`), lastSeq], in order per pixel.

@@ -421,18 +421,25 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     unsigned poolNext = 64;
     WaveWords *const ww = reinterpret_cast<WaveWords *>(pool - kWW);
     ChainWave *const cw = &ww->cw;
-    ChainView *const view = &reinterpret_cast<WaveWords *>(reinterpret_cast<char *>(lds) + P.poolOffset)->view;
+    WaveWords *const bw = reinterpret_cast<WaveWords *>(reinterpret_cast<char *>(lds) + P.poolOffset);
+    ChainView *const view = &bw->view;
+#ifdef HIPPT_EXP_NODRAINED
+    unsigned *const drained = POOL && CHAIN ? bw->drained : nullptr;
+#else
+    unsigned *const drained = POOL ? bw->drained : nullptr;  // the block's drained-queue words
+#endif
     // CHAIN kernels keep the work queue and the segment count in LDS (ww->Q, ww->segs), the others in
     // registers
     WorkQueue Q;
+    if (POOL && threadIdx.x == 0) bw->drained[0] = bw->drained[1] = 0u;
     if constexpr (CHAIN) {
         chain_begin(Q, cw, view);
         store_queue(&ww->Q, Q);
         if (__lane_id() == 0) ww->segs = 0;
-        __syncthreads();  // the block's mailbox view (its first wave's) is initialised
     } else {
         queue_begin(Q, P.totalItems, P.chunk);
     }
+    if (POOL) __syncthreads();  // the block's words (its first wave's: mailbox view, drained queues)
     unsigned item = kNone;
     uint32_t rng = 0;
     int depth = 0;
@@ -535,7 +542,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                             const unsigned got =
                                 queue_fetch(want, Q, chain_block(late_field(chainCtl), t, late_field(chainSlots)),
                                             late_field(totalItems), late_field(chunk),
-                                            t == __builtin_amdgcn_readfirstlane(cw->stat));
+                                            t == __builtin_amdgcn_readfirstlane(cw->stat), drained, t);
                             if (want && got != kNone) {
                                 raw = got;
                                 tItem = t;
@@ -553,8 +560,8 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                             it |= (tItem & (late_field(chainSlots) - 1u)) << late_field(chainShift);
                         }
                     } else {
-                        it = HIPPT_LATE_CAM ? order_item_late(queue_fetch(true, Q, P.queue, P.totalItems, P.chunk))
-                                            : order_item(P, queue_fetch(true, Q, P.queue, P.totalItems, P.chunk));
+                        it = HIPPT_LATE_CAM ? order_item_late(queue_fetch(true, Q, P.queue, P.totalItems, P.chunk, true, drained))
+                                            : order_item(P, queue_fetch(true, Q, P.queue, P.totalItems, P.chunk, true, drained));
                         if (it != kNone) {
                             if (HIPPT_LATE_CAM)
                                 camera_sample(cam_args_late(), it, c, crng);

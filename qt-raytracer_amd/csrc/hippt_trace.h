@@ -178,11 +178,30 @@ __device__ __forceinline__ void queue_begin(WorkQueue &Q, unsigned total, unsign
     Q.end = min(Q.next + chunk, Q.qEnd);
 }
 
+// A queue found drained, for the block (LDS word drained[t & 1] = t << 8 | one bit per queue of
+// batch t), so that the block's other waves skip it: at a batch's end every wave otherwise learns
+// each queue's end by one failing atomic on its counter, and those atomics serialise on the
+// counter's line (~11 ns each, MI355X_MICROARCH.md "dequeue"): 7168 waves x 8 queues held a chained
+// launch's waves ~50 us at each batch boundary (r5k rate timeline).
+__device__ __forceinline__ void block_drained_set(unsigned *drained, unsigned t, unsigned g) {
+    unsigned *const w = &drained[t & 1u];
+    unsigned old = __hip_atomic_load(w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    for (;;) {
+        if ((old >> 8) > t) return;  // the word holds a later batch
+        const unsigned nw = ((old >> 8) == t ? old : (t << 8)) | (1u << g);
+        if (nw == old ||
+            __hip_atomic_compare_exchange_strong(w, &old, nw, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))
+            return;
+    }
+}
+
 // One item per requesting lane (kNone once every queue is drained).  Whole wave, uniform
 // control flow; the pool and queue state are wave-uniform.  stat: the queues have static first
-// chunks (queue_begin); a chained batch a launch moves into has none (chain_select).
+// chunks (queue_begin); a chained batch a launch moves into has none (chain_select).  drained
+// (camera-pool kernels): the block's drained-queue words (block_drained_set) for batch t.
 __device__ __forceinline__ unsigned queue_fetch(bool req, WorkQueue &Q, unsigned *ctr, unsigned total,
-                                                unsigned chunk, bool stat = true) {
+                                                unsigned chunk, bool stat = true, unsigned *drained = nullptr,
+                                                unsigned t = 0) {
     unsigned item = kNone;
     bool want = req;
     unsigned long long m = __ballot(want);
@@ -196,20 +215,32 @@ __device__ __forceinline__ unsigned queue_fetch(bool req, WorkQueue &Q, unsigned
     while (Q.left && __ballot(want)) {
         m = __ballot(want);
         rank = __builtin_amdgcn_mbcnt_hi(unsigned(m >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(m), 0u));
-        const unsigned c = Q.qEnd - min(Q.end, Q.qEnd) < Q.waves * chunk ? kTailChunk : chunk;
-        unsigned base = 0;
-        if (__lane_id() == 0) base = atomicAdd(&ctr[Q.g * kQueueStride], c);
-        base = __builtin_amdgcn_readfirstlane(base) + Q.dynBase;
-        if (base < Q.qEnd) {
-            Q.next = base;
-            Q.end = min(base + c, Q.qEnd);
-            avail = Q.end - Q.next;
-            if (want && rank < avail) {
-                item = Q.next + rank;
-                want = false;
+        bool gone = false, got = false;
+        if (drained) {
+            const unsigned w = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(&drained[t & 1u], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
+            gone = (w >> 8) == t && ((w >> Q.g) & 1u);
+        }
+        if (!gone) {
+            const unsigned c = Q.qEnd - min(Q.end, Q.qEnd) < Q.waves * chunk ? kTailChunk : chunk;
+            unsigned base = 0;
+            if (__lane_id() == 0) base = atomicAdd(&ctr[Q.g * kQueueStride], c);
+            base = __builtin_amdgcn_readfirstlane(base) + Q.dynBase;
+            if (base < Q.qEnd) {
+                got = true;
+                Q.next = base;
+                Q.end = min(base + c, Q.qEnd);
+                avail = Q.end - Q.next;
+                if (want && rank < avail) {
+                    item = Q.next + rank;
+                    want = false;
+                }
+                Q.next += min(unsigned(__popcll(m)), avail);
+            } else if (drained && __lane_id() == 0) {
+                block_drained_set(drained, t, Q.g);
             }
-            Q.next += min(unsigned(__popcll(m)), avail);
-        } else if (--Q.left) {
+        }
+        if (!got && --Q.left) {
             queue_select(Q, Q.g + 1 == kQueues ? 0u : Q.g + 1, total, chunk);
             if (!stat) Q.dynBase = queue_start(total, Q.g);
             Q.next = Q.end = 0;
@@ -378,7 +409,8 @@ struct WaveWords {
     WorkQueue Q;
     unsigned segs;
     ChainWave cw;
-    ChainView view;  // (the block's first wave's only)
+    ChainView view;       // (the block's first wave's only)
+    unsigned drained[2];  // (the block's first wave's only: queue_fetch's block_drained_set words)
 };
 static_assert(sizeof(WaveWords) == kWaveWords * 4, "per-wave LDS words");
 
