@@ -186,7 +186,14 @@ struct Ctx {
         unsigned slots = 0, shift = 0, cap = 0;
         hippt::MeshParams key{};  // what every batch of the run shares (chain_same)
         long long blocks = 0;
+        unsigned lastOwn = 0;     // the batch of the run's last enqueued launch
+        // a batch posted without a launch of its own (chain_batch: the last enqueued launch had not
+        // started, so it takes the batch): its parameters, launched by flush_chain if the run ends
+        // before another launch (a launch of the run still to start then finds the run closed)
+        bool pend = false;
+        hippt::MeshParams pendP{};
     } chain;
+    hipEvent_t chainStartEv = nullptr;  // recorded before each chained launch (chain_batch's skip test)
     unsigned *chainCtl = nullptr;
     float *chainScratch = nullptr;
     size_t chainScratchBytes = 0;
@@ -428,6 +435,7 @@ void destroy_ctx(Ctx &c) {
     (void)hipFree(c.chainCtl);
     (void)hipFree(c.chainScratch);
     if (c.chainBox) (void)hipHostFree(c.chainBox);
+    if (c.chainStartEv) (void)hipEventDestroy(c.chainStartEv);
     (void)hipFree(c.stats);
     (void)hipFree(c.wfPool);
     (void)hipFree(c.wfCtr);
@@ -969,11 +977,19 @@ bool copy_rows_async(Ctx &c, void *dstFrame, const void *src, size_t bytes, cons
 
 // The open chain run's last combines (Ctx::chain): every batch no launch combined, in order; the run
 // ends (the next chained batch starts a new one).
+bool launch_chained(Ctx &c, hippt::MeshParams &p, const char **err);
+
 bool flush_chain(Ctx &c, const char **err) {
     Ctx::Chain &ch = c.chain;
     if (!ch.live) return true;
-    ch.live = false;
     HIP_TRY(hipSetDevice(c.device));
+    if (ch.pend) {
+        // before the run closes: the launch its batches since the last launch would have had, from the
+        // first of them through the last posted (the last launch, yet to start, may find the run closed)
+        ch.pendP.chainPosted = ch.seq - 1u;
+        if (!launch_chained(c, ch.pendP, err)) return false;
+    }
+    ch.live = false;
     hippt::ChainFlushParams f{};
     f.comb = ch.key.comb;
     f.scratch = c.chainScratch;
@@ -1031,6 +1047,11 @@ bool batch_scratch(Ctx &c, size_t need, float **out, const char **err) {
 // launch traces one group of batches while it combines the previous one.
 // automatic (HIPPT_OPT_CHAIN -1): chained batches on or off
 constexpr bool kChainAuto = false;
+// chain_batch's launch skip (an A/B build knob)
+#ifndef HIPPT_CHAIN_SKIP
+#define HIPPT_CHAIN_SKIP 1
+#endif
+constexpr bool kChainSkip = HIPPT_CHAIN_SKIP != 0;
 
 unsigned chain_cap(long long option, unsigned total) {
     if (option > 0) return unsigned(std::min<long long>(option, 8));
@@ -1063,9 +1084,32 @@ bool chain_same(const hippt::MeshParams &a, const hippt::MeshParams &b) {
            a.poolWords == b.poolWords && a.comb.format == b.comb.format;
 }
 
+// Enqueues the launch of chained batch p (its chain fields set by chain_batch but the epoch): the run's
+// next launch number, and the start event chain_batch's skip test queries.
+bool launch_chained(Ctx &c, hippt::MeshParams &p, const char **err) {
+    Ctx::Chain &ch = c.chain;
+    p.chainEpoch = ch.epoch++;
+    ch.lastOwn = p.chainSeq;
+    ch.pend = false;
+    if (!c.chainStartEv) HIP_TRY(hipEventCreateWithFlags(&c.chainStartEv, hipEventDisableTiming));
+    EventPair ev;
+    if (!next_events(c, ev, err)) return false;
+    HIP_TRY(hipEventRecord(c.chainStartEv, c.stream));
+    HIP_TRY(hipEventRecord(ev.a, c.stream));
+    HIP_TRY(hippt::launch_mesh(p, int(ch.blocks), false, c.stream));
+    HIP_TRY(hipEventRecord(ev.b, c.stream));
+    c.pending.push_back({0, ev});
+    return true;
+}
+
 // Makes batch `p` (its parameters otherwise complete, `blocks` its grid) the next batch of the open
-// run, or of a new run (the old one flushed first): the chain fields, the ring slot's scratch, and
-// the mailbox post.
+// run, or of a new run (the old one flushed first): the chain fields, the ring slot's scratch, the
+// mailbox post, and the launch.  The launch is skipped when the run's last enqueued launch has not
+// started yet and may trace this batch (within chainCap of its own): posted before that launch
+// starts, the batch is taken by it (a wave leaves a run only at the launch's last batch or at a batch
+// not yet posted), so the launch it would have had could only combine.  Without the skip, a burst of
+// async batches leaves one such combine-only launch per batch behind each tracing launch (~21 us
+// each, plus the gap between launches; r5j).
 bool chain_batch(Ctx &c, hippt::MeshParams &p, long long blocks, long long option, const char **err) {
     Ctx::Chain &ch = c.chain;
     p.comb = hippt::CombineParams{c.accum, c.out, nullptr, p.bandPixels, p.totalItems, 0, p.frames, p.comb.format};
@@ -1110,6 +1154,8 @@ bool chain_batch(Ctx &c, hippt::MeshParams &p, long long blocks, long long optio
         ch.run = (ch.run + 1u) & 0x7fffffffu;
         ch.seq = 0;
         ch.epoch = 0;
+        ch.lastOwn = 0;
+        ch.pend = false;
         ch.firstFrame = p.firstFrame;
         ch.step = -1;
         ch.slots = slots;
@@ -1128,19 +1174,28 @@ bool chain_batch(Ctx &c, hippt::MeshParams &p, long long blocks, long long optio
     p.chainCtl = c.chainCtl;
     p.chainBox = c.chainBoxDev;
     p.chainSeq = ch.seq;
-    p.chainEpoch = ch.epoch;
     p.chainRun = ch.run;
     p.chainSlots = ch.slots;
     p.chainShift = ch.shift;
     p.chainCap = ch.cap;
     p.chainStep = ch.step;
+    p.chainPosted = ch.seq;
     // post: one word, so that a launch reads the run, its frame pattern and the last batch together
     const unsigned long long consecutive = ch.step > 0 ? 1u : 0u;
     __atomic_store_n(c.chainBox, ((unsigned long long)ch.run << 33) | (consecutive << 32) | ch.seq, __ATOMIC_RELEASE);
-    ++ch.seq;
-    ++ch.epoch;
     c.hostSamples += p.totalItems;
-    return true;
+    // (the query after the post: a launch found not started reads the mailbox after it)
+    const bool skip = ch.epoch > 0 && ch.seq <= ch.lastOwn + ch.cap - 1u && kChainSkip &&
+                      hipEventQuery(c.chainStartEv) == hipErrorNotReady;
+    ++ch.seq;
+    if (skip) {
+        if (!ch.pend) {  // the run's first batch without a launch since its last launch
+            ch.pend = true;
+            ch.pendP = p;
+        }
+        return true;
+    }
+    return launch_chained(c, p, err);
 }
 
 // The device address of a mapped pinned host frame on the current device, or null where the
@@ -1409,6 +1464,8 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                             if (chained) {
                                 p.comb.format = s.pixelFormat;
                                 if (!chain_batch(c, p, blocks, s.chainBatches, err)) return false;
+                                continue;  // launched or taken by the run's last launch; its combine
+                                           // belongs to the run (Ctx::chain)
                             } else {
                                 HIP_TRY(hipMemsetAsync(c.queue, 0, kQueueBytes, c.stream));
                                 if (c.hasDeferred) {

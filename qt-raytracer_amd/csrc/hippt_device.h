@@ -126,6 +126,7 @@ struct MeshParams {
     unsigned chainSeq, chainEpoch, chainRun;
     unsigned chainSlots, chainShift, chainCap;
     int chainStep;
+    unsigned chainPosted;  // the run's last batch posted when the launch was enqueued (>= chainSeq)
 };
 
 // Chained batches: the control block (unsigned words).  Ring slot k's block at k * kChainBlockWords:

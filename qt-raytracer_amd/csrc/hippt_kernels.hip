@@ -898,7 +898,8 @@ hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hip
     const bool chain = p.chainCtl != nullptr;
     if (chain && (!p.chainBox || p.chainSlots < 2 || p.chainSlots > kChainSlotsMax || (p.chainSlots & (p.chainSlots - 1)) ||
                   p.chainShift > kChainMaxShift || p.totalItems > (1u << p.chainShift) || p.chainCap < 1 ||
-                  p.chainCap >= p.chainSlots || p.comb.bandPixels != p.bandPixels || p.comb.frames != p.frames))
+                  p.chainCap >= p.chainSlots || p.chainPosted < p.chainSeq || p.chainPosted - p.chainSeq >= p.chainCap ||
+                  p.comb.bandPixels != p.bandPixels || p.comb.frames != p.frames))
         return hipErrorInvalidValue;
     const size_t bytes = mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0, p.wide != 0, p.topBytes,
                                         lds ? p.numMats : 0, p.poolWords);

@@ -457,6 +457,7 @@ __device__ __forceinline__ void chain_select(WorkQueue &Q, unsigned g, unsigned 
 __device__ __forceinline__ void chain_begin(WorkQueue &Q, ChainWave *cw, ChainView *view) {
     unsigned *const ctl = late_field(chainCtl);
     const unsigned e = late_field(chainEpoch), own = late_field(chainSeq), R = late_field(chainSlots);
+    const unsigned posted = late_field(chainPosted);
     const unsigned total = late_field(totalItems), chunk = late_field(chunk);
     // the first batch not combined by an earlier launch (written at the previous launch's start)
     const unsigned c0 = __builtin_amdgcn_readfirstlane(ctl[kChainCtlWord + 32u * ((e + 1u) & 1u)]);
@@ -480,12 +481,12 @@ __device__ __forceinline__ void chain_begin(WorkQueue &Q, ChainWave *cw, ChainVi
         cw->c0 = c0;
         cw->c1 = unsigned(c1);
         cw->tLim = tLim;
-        cw->posted = own + 1u;  // the own batch is posted before its launch is enqueued
+        cw->posted = posted + 1u;  // posted before the launch was enqueued
         cw->step = step;
         cw->t = u == own ? own : u - 1u;
         cw->stat = u == own ? own : ~0u;
         if (threadIdx.x == 0) {
-            view->last = own;
+            view->last = posted;
             view->flags = step > 0 ? 1u : 0u;
             view->stamp = 0;
             view->busy = 0;
@@ -523,10 +524,10 @@ __device__ __forceinline__ void chain_begin(WorkQueue &Q, ChainWave *cw, ChainVi
 // then reads the copy once more.  Stale answers only ever say "not yet posted": a wave then stops
 // taking batches, and a later launch traces them.
 __device__ __forceinline__ void chain_copy_pack(unsigned long long now, unsigned long long h, unsigned run,
-                                                unsigned long long &c) {
+                                                unsigned ep, unsigned long long &c) {
     // the host on a later run: this one is closed (and the word's batch is that run's)
     const bool closed = unsigned(h >> 33) != run;
-    c = ((now >> 4) << 40) | (closed ? (1ull << 33) : (h & ((1ull << 33) - 1ull)));
+    c = ((now >> 4) << 40) | ((unsigned long long)ep << 34) | (closed ? (1ull << 33) : (h & ((1ull << 33) - 1ull)));
 }
 __device__ __forceinline__ void chain_ask(unsigned nt, ChainView *view, unsigned &last, unsigned &flags) {
     constexpr unsigned long long kBoxRefresh = 1000;  // 10 us of the 100 MHz clock
@@ -554,15 +555,21 @@ __device__ __forceinline__ void chain_ask(unsigned nt, ChainView *view, unsigned
                                                                           (blockIdx.x % kQueues) * 32u);
     unsigned long long *const copy = box, *const claim = box + 1;
     const unsigned run = late_field(chainRun);
+    // the copy and the claim carry the launch (epoch mod 64) that made them: a copy made by an earlier
+    // launch says nothing about batches posted since, and chain_batch posts batches without a launch
+    // of their own only before the launch that is to take them starts (so its negative must be fresh)
+    const unsigned ep = late_field(chainEpoch) & 63u;
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
     unsigned long long c = __hip_atomic_load(copy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned age = (unsigned(now >> 4) - unsigned(c >> 40)) & 0xffffffu;  // in 16-tick units
-    if (unsigned(c) < nt && !((c >> 33) & 1ull) && age >= kBoxRefresh / 16u) {
-        unsigned long long prev = __hip_atomic_load(claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (now - prev >= kBoxRefresh && atomicCAS(claim, prev, now) == prev) {  // this wave refreshes
+    const bool ours = (unsigned(c >> 34) & 63u) == ep;
+    if (unsigned(c) < nt && !((c >> 33) & 1ull) && (!ours || age >= kBoxRefresh / 16u)) {
+        const unsigned long long prev = __hip_atomic_load(claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const bool active = (unsigned(prev) & 63u) == ep && now - (prev & ~63ull) < kBoxRefresh;
+        if (!active && atomicCAS(claim, prev, (now & ~63ull) | ep) == prev) {  // this wave refreshes
             const unsigned long long h =
                 __hip_atomic_load(late_field(chainBox), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            chain_copy_pack(__builtin_amdgcn_s_memrealtime(), h, run, c);
+            chain_copy_pack(__builtin_amdgcn_s_memrealtime(), h, run, ep, c);
             __hip_atomic_store(copy, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {  // a refresh is in flight (claimed at most kBoxRefresh ago): give it 4 us, read once more
             while (__builtin_amdgcn_s_memrealtime() - now < 400u) __builtin_amdgcn_s_sleep(8);
