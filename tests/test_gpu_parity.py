@@ -727,6 +727,37 @@ def test_chained_batches_camera_change_and_row_shares(pt):
     pt.setRowRange(0, 0)
 
 
+def test_chained_batches_with_skipped_launches(pt):
+    """chain_batch posts a batch without a launch of its own while the run's last launch has not
+    started (that launch takes it); a run that closes with such batches (a camera change, a readback)
+    gets one catch-up launch.  Batches long enough (256 frames of 96x54) that each launch is still
+    queued behind the running one when the next batches are posted: the images equal one launch per
+    batch, before and after a camera change, and the sample count is exact."""
+    import ctypes
+    sc = scenes.cornell34()
+    w, h = 96, 54
+    lib = hippt.load_library()
+    moved = dict(lookfrom=(sc.lookfrom[0] - 30.0, sc.lookfrom[1] + 20.0, sc.lookfrom[2]), lookat=sc.lookat,
+                 vup=sc.vup, vfov=sc.vfov, aspect=w / h, aperture=sc.aperture, focus=sc.focus)
+    err = ctypes.c_char_p()
+    images = {}
+    for chain in (0, 8, 3):
+        pt.setOption(hippt.OPT_CHAIN, chain)
+        pt.uploadMesh(sc)
+        assert pt.initialize(w, h)
+        pt.resetStats()
+        for _ in range(11):  # progressive batches: frames 0..2815
+            assert pt.renderFramesAsync(256, 8), pt.lastError()
+        cam = hippt.build_camera(**moved)
+        assert lib.hipptSetCamera(ctypes.byref(cam), ctypes.byref(err)), err.value
+        for _ in range(5):  # the same frames again: every batch restarts the average
+            assert lib.hipptRenderFramesAsync(0, 256, 8, None)
+        images[chain] = pt.readback()
+        assert pt.stats()["pixelSamples"] == w * h * 256 * 16
+    for chain in (8, 3):
+        _assert_same(images[chain][0], images[chain][1], images[0][0], images[0][1])
+
+
 @pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene"])
 def test_deferred_combine_across_async_calls(pt, name):
     """Back-to-back hipptRenderFramesAsync calls: each megakernel batch's combine (running average
