@@ -987,6 +987,10 @@ bool flush_chain(Ctx &c, const char **err) {
         // before the run closes: the launch its batches since the last launch would have had, from the
         // first of them through the last posted (the last launch, yet to start, may find the run closed)
         ch.pendP.chainPosted = ch.seq - 1u;
+#ifdef HIPPT_CHAIN_TRACE
+        std::fprintf(stderr, "chain run %u catch-up own %u posted %u epoch %u\n", ch.run, ch.pendP.chainSeq,
+                     ch.pendP.chainPosted, ch.epoch);
+#endif
         if (!launch_chained(c, ch.pendP, err)) return false;
     }
     ch.live = false;
@@ -1106,10 +1110,12 @@ bool launch_chained(Ctx &c, hippt::MeshParams &p, const char **err) {
 // run, or of a new run (the old one flushed first): the chain fields, the ring slot's scratch, the
 // mailbox post, and the launch.  The launch is skipped when the run's last enqueued launch has not
 // started yet and may trace this batch (within chainCap of its own): posted before that launch
-// starts, the batch is taken by it (a wave leaves a run only at the launch's last batch or at a batch
-// not yet posted), so the launch it would have had could only combine.  Without the skip, a burst of
-// async batches leaves one such combine-only launch per batch behind each tracing launch (~21 us
-// each, plus the gap between launches; r5j).
+// starts, the batch is normally taken by it (a wave leaves a run only at the launch's last batch or
+// at a batch not yet posted), so the launch it would have had could only combine.  Without the skip,
+// a burst of async batches leaves one such combine-only launch per batch behind each tracing launch
+// (~21 us each, plus the gap between launches; r5j).  The next launch of the run (or the run's
+// catch-up launch in flush_chain) starts at the first skipped batch, so a skipped batch the last
+// launch did not take is traced there.
 bool chain_batch(Ctx &c, hippt::MeshParams &p, long long blocks, long long option, const char **err) {
     Ctx::Chain &ch = c.chain;
     p.comb = hippt::CombineParams{c.accum, c.out, nullptr, p.bandPixels, p.totalItems, 0, p.frames, p.comb.format};
@@ -1187,6 +1193,10 @@ bool chain_batch(Ctx &c, hippt::MeshParams &p, long long blocks, long long optio
     // (the query after the post: a launch found not started reads the mailbox after it)
     const bool skip = ch.epoch > 0 && ch.seq <= ch.lastOwn + ch.cap - 1u && kChainSkip &&
                       hipEventQuery(c.chainStartEv) == hipErrorNotReady;
+#ifdef HIPPT_CHAIN_TRACE
+    std::fprintf(stderr, "chain run %u seq %u %s (lastOwn %u epoch %u cap %u slots %u)\n", ch.run, ch.seq,
+                 skip ? "skipped" : "launched", ch.lastOwn, ch.epoch, ch.cap, ch.slots);
+#endif
     ++ch.seq;
     if (skip) {
         if (!ch.pend) {  // the run's first batch without a launch since its last launch
@@ -1194,6 +1204,15 @@ bool chain_batch(Ctx &c, hippt::MeshParams &p, long long blocks, long long optio
             ch.pendP = p;
         }
         return true;
+    }
+    if (ch.pend) {
+        // The batches posted without a launch since the last one: this launch starts at the first of
+        // them (its own) and knows them all posted, so that it traces whatever the last launch did not
+        // take.  (The skip only expects the last launch to take them; the image never depends on it,
+        // nor on when the host saw that launch start.)
+        hippt::MeshParams q = ch.pendP;
+        q.chainPosted = p.chainSeq;
+        return launch_chained(c, q, err);
     }
     return launch_chained(c, p, err);
 }
