@@ -537,14 +537,18 @@ def main():
                 "combine_ms_per_step": round(st["combineMs"] / args.steps, 4),
                 "bvh_nodes": st["bvhNodes"], "bvh_depth": st["bvhDepth"], "bvh_width": bvh_width,
                 "wave_threshold": pt._lib.hipptGetOption(hippt.OPT_WAVE_THRESHOLD),
-                "chunk": pt._lib.hipptGetOption(hippt.OPT_CHUNK),
+                "chunk": {"option": pt._lib.hipptGetOption(hippt.OPT_CHUNK),
+                          "applied": pt._lib.hipptGetOption(hippt.INFO_CHUNK)},
                 "image_crc32": image_crc,
                 # the library default is -1 (automatic: the estimate on a host thread, batches queued
                 # meanwhile in image order); bench.py forces it
                 "chain": {"option": pt._lib.hipptGetOption(hippt.OPT_CHAIN),
-                          "note": "HIPPT_OPT_CHAIN (default -1, automatic): one launch is enqueued per step; "
-                                  "a launch whose batch is drained goes on with the steps posted behind it "
-                                  "(ring of batches, hippt_trace.h), the next launch combines them; every "
+                          "applied_cap": pt._lib.hipptGetOption(hippt.INFO_CHAIN_CAP),
+                          "note": "HIPPT_OPT_CHAIN (default -1, automatic: chained for batches of at most "
+                                  "2^26 samples and for trees in global memory): a launch whose batch is "
+                                  "drained goes on with the steps posted behind it (ring of batches, "
+                                  "hippt_trace.h), a later launch combines them, and a step posted before "
+                                  "the run's last launch has started gets no launch of its own; every "
                                   "step's frames are traced and combined inside the timed region"},
                 "item_order": {"option": 1, "library_default": -1,
                                "note": "run-cost estimate computed on the first (counted, untimed) call, "

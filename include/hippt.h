@@ -183,7 +183,9 @@ enum {
     HIPPT_OPT_WAVE_THRESHOLD = 2,   /* lanes still traversing below which a wave goes to shade; -1 (default):
                                        16 for LDS-resident scenes, 32 otherwise */
     HIPPT_OPT_SCRATCH_MB = 3,       /* cap of the per-batch sample scratch per device (32768: one batch for 4K x 256 spp) */
-    HIPPT_OPT_CHUNK = 4,            /* work items a wave takes from the global queue at once */
+    HIPPT_OPT_CHUNK = 4,            /* work items a wave takes from the global queue at once (64..2^20, a
+                                       multiple of 64); 0 (default): automatic, 512 for whole-image batches
+                                       (>= 2^26 samples) of the Lambertian megakernel, else 256 */
     HIPPT_OPT_BLOCKS_PER_CU = 5,    /* persistent-grid residency (0 = occupancy query) */
     HIPPT_OPT_LDS_SCENE = 6,        /* 1 (default): small scenes are copied into LDS per block */
     HIPPT_OPT_PATH_MODE = 8,        /* 0 (default): persistent megakernel; 1: wavefront kernels */
@@ -251,7 +253,8 @@ enum {
                                        many (1..8), so that the run pays the launch's tail once per that many
                                        batches; the next launch combines them beside its own paths and the
                                        image's readers flush the rest.  0: one launch per batch; -1
-                                       (default): automatic (on, 2..8 batches by the batch's size).  Same
+                                       (default): automatic (on for batches of at most 2^26 samples and for
+                                       trees in global memory, 2..8 batches by the batch's size).  Same
                                        results either way */
 };
 /* Output frame word formats (HIPPT_OPT_PIXEL_FORMAT).  Both map an accumulated colour c to
@@ -263,8 +266,10 @@ enum {
  *          VulkanPathTracer::hostPixels) backends store. */
 enum { HIPPT_PIXEL_ARGB = 0, HIPPT_PIXEL_RGBA8 = 1 };
 /* Read-only (hipptGetOption) facts of the last megakernel render: LDS bytes of the top of the tree,
- * persistent-grid blocks per CU. */
-enum { HIPPT_INFO_LDS_TOP_BYTES = 100, HIPPT_INFO_BLOCKS_PER_CU = 101 };
+ * persistent-grid blocks per CU, work items per claim (HIPPT_OPT_CHUNK as applied), batches a launch
+ * may trace (HIPPT_OPT_CHAIN as applied: 0 = the batch was not chained). */
+enum { HIPPT_INFO_LDS_TOP_BYTES = 100, HIPPT_INFO_BLOCKS_PER_CU = 101, HIPPT_INFO_CHUNK = 102,
+       HIPPT_INFO_CHAIN_CAP = 103 };
 bool hipptSetOption(int key, long long value);
 long long hipptGetOption(int key);
 /* BVH width (2 or 4) the last mesh render traversed (0 before any): what nodeVisits count. */

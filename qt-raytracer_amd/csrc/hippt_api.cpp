@@ -254,7 +254,7 @@ struct State {
     int waveThreshold = -1;  // -1: automatic (16 for LDS scenes, 32 for trees in global memory)
     // one batch (and one end-of-batch tail) per call up to 4K/256 spp: 2.12G samples x 12 B
     long long scratchMB = 32768;
-    unsigned chunk = 256;
+    unsigned chunk = 0;  // work items per claim (0: automatic, see enqueue_locked)
     int leafExit = -1;  // -1: automatic from the tree depth and LDS residency
     int nodeExit = -1;  // -1: automatic
     int bvhWidth = 0;   // megakernel traversal over the 2- or 4-wide BVH; 0: 4-wide if it fits in LDS
@@ -270,6 +270,8 @@ struct State {
     std::vector<std::pair<int, uint32_t *>> rngTables;  // per device, built on first use
     unsigned activeTopBytes = 0;  // of the last mesh render (hipptGetOption HIPPT_INFO_*)
     int activeBlocksPerCu = 0;
+    int activeChunk = 0;     // the last megakernel batch's claim size
+    int activeChainCap = 0;  // its run's chain cap (0: not chained)
     int activeWidth = 0;  // BVH width of the last mesh render (hipptActiveBvhWidth)
     int blocksPerCu = 0;
     bool ldsScene = true;
@@ -1049,8 +1051,14 @@ bool batch_scratch(Ctx &c, size_t need, float **out, const char **err) {
 // Chained batches (Ctx::chain).  Automatic: a launch traces up to ~4e8 samples' worth of batches (3 of
 // a whole 1080p/64 spp image, 8 of its 1/4 and 1/8 row shares); the ring holds twice that, so that a
 // launch traces one group of batches while it combines the previous one.
-// automatic (HIPPT_OPT_CHAIN -1): chained batches on or off
-constexpr bool kChainAuto = false;
+// Automatic (HIPPT_OPT_CHAIN -1): chained batches for every batch of at most 2^26 samples (the row
+// shares of a 1080p/64 spp image split over 2 or more GPUs) and for trees in global memory; a whole
+// image of an LDS-resident scene runs one launch per batch.  Measured (r5s, 20 steps, cap by
+// chain_cap): 1/8 shares Cornell 1.112 -> 1.047 ms, blob70k 3.003 -> 2.518, cornell_mixed 1.831 ->
+// 1.573; 1/2 shares blob70k 9.79 -> 9.49, cornell_mixed 6.20 -> 5.92, Cornell 3.757 -> 3.765; whole
+// images blob70k 18.94 -> 18.69, but Cornell 7.255 -> 7.321: a whole Cornell batch has little tail to
+// save, and a run pays its first launch's start and its last group's combine without overlap.
+bool chain_auto(unsigned total, bool ldsScene) { return total <= (1u << 26) || !ldsScene; }
 // chain_batch's launch skip (an A/B build knob)
 #ifndef HIPPT_CHAIN_SKIP
 #define HIPPT_CHAIN_SKIP 1
@@ -1384,7 +1392,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                     const bool fuse = maxDepth > 0 && s.pathMode == 0 && s.fuseCombine != 0;
                     // chained batches (Ctx::chain): asynchronous camera-pool megakernel batches over
                     // 4-wide float nodes whose items fit the ring's slot bits
-                    const bool chained = fuse && !copy && !cnt && (s.chainBatches > 0 || (s.chainBatches < 0 && kChainAuto)) &&
+                    const bool chained = fuse && !copy && !cnt && (s.chainBatches > 0 || (s.chainBatches < 0 && chain_auto(total, ldsScene))) &&
                                          poolWords != 0 &&
                                          fmt == hippt::kWideFloat && c.meshBlocksPerCuChain > 0 &&
                                          total <= (1u << hippt::kChainMaxShift);
@@ -1433,7 +1441,13 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         // +5.8% over 32 with the exits below, r6c)
                         const bool fullMega = s.pathMode == 0 && s.scene.full;
                         p.waveThreshold = s.waveThreshold >= 0 ? s.waveThreshold : ldsScene || fullMega ? 24 : 32;
-                        p.chunk = s.chunk;
+                        // claim size: 512 items for whole-image batches of the Lambertian kernels
+                        // (Cornell 1080p/64 spp 7.255 -> 7.199 ms, blob70k 18.94 -> 18.91, r5s); 256
+                        // for smaller batches (1/8 shares: Cornell 1.112 -> 1.137 and blob70k 3.00 ->
+                        // 3.22 with 512) and the general kernel (cornell_mixed 12.06 -> 12.22)
+                        p.chunk = s.chunk > 0                                                   ? s.chunk
+                                  : s.pathMode == 0 && !s.scene.full && total >= (1u << 26) ? 512u
+                                                                                             : 256u;
                         // Loop exits of the traversal round (measured): trees in global
                         // memory leave the node loop once <= 17 lanes still search for a leaf (r2
                         // sweep of the 4-wide kernels: blob70k, 21 levels, best at 17-18; blob64x34
@@ -1480,9 +1494,12 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                             blocks = std::min<long long>(blocks, (total + hippt::kMeshBlock - 1) / hippt::kMeshBlock);
                             blocks = std::max<long long>(blocks, 1);
                             if (!ensure_spill(c, p, blocks, spills, s.scene.stackBound4 + 3, err)) return false;
+                            s.activeChunk = int(p.chunk);
+                            s.activeChainCap = 0;
                             if (chained) {
                                 p.comb.format = s.pixelFormat;
                                 if (!chain_batch(c, p, blocks, s.chainBatches, err)) return false;
+                                s.activeChainCap = int(c.chain.cap);
                                 continue;  // launched or taken by the run's last launch; its combine
                                            // belongs to the run (Ctx::chain)
                             } else {
@@ -2134,7 +2151,7 @@ extern "C" bool hipptSetOption(int key, long long value) try {
         s.scratchMB = value;
         return true;
     case HIPPT_OPT_CHUNK:
-        if (value < 64 || value > (1 << 20) || value % 64) return false;
+        if (value != 0 && (value < 64 || value > (1 << 20) || value % 64)) return false;
         s.chunk = unsigned(value);
         return true;
     case HIPPT_OPT_BLOCKS_PER_CU:
@@ -2286,6 +2303,8 @@ extern "C" long long hipptGetOption(int key) try {
     case HIPPT_OPT_CHAIN: return s.chainBatches;
     case HIPPT_INFO_LDS_TOP_BYTES: return s.activeTopBytes;
     case HIPPT_INFO_BLOCKS_PER_CU: return s.activeBlocksPerCu;
+    case HIPPT_INFO_CHUNK: return s.activeChunk;
+    case HIPPT_INFO_CHAIN_CAP: return s.activeChainCap;
     default: return -1;
     }
 } catch (const std::exception &e) {

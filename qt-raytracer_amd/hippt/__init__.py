@@ -59,6 +59,8 @@ PIXEL_ARGB = 0
 PIXEL_RGBA8 = 1
 INFO_LDS_TOP_BYTES = 100
 INFO_BLOCKS_PER_CU = 101
+INFO_CHUNK = 102
+INFO_CHAIN_CAP = 103
 
 # Every symbol include/hippt.h declares (checked by tests/test_abi_cpu.py).
 EXPORTS = (

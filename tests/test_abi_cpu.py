@@ -76,6 +76,9 @@ def test_options_validate():
     assert lib.hipptGetOption(hippt.OPT_WAVE_THRESHOLD) == 8
     assert not lib.hipptSetOption(hippt.OPT_WAVE_THRESHOLD, 65)
     assert not lib.hipptSetOption(hippt.OPT_CHUNK, 100)
+    assert lib.hipptGetOption(hippt.OPT_CHUNK) == 0  # automatic (enqueue_locked)
+    assert lib.hipptSetOption(hippt.OPT_CHUNK, 512) and lib.hipptGetOption(hippt.OPT_CHUNK) == 512
+    assert lib.hipptSetOption(hippt.OPT_CHUNK, 0) and lib.hipptGetOption(hippt.OPT_CHUNK) == 0
     assert not lib.hipptSetOption(999, 1)
     assert lib.hipptSetOption(hippt.OPT_WAVE_THRESHOLD, -1)
     assert not lib.hipptSetOption(hippt.OPT_WAVE_THRESHOLD, -2)

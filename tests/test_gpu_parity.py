@@ -23,7 +23,7 @@ def pt():
     t.setRowRange(0, 0)
     t.setOption(hippt.OPT_DEVICE_ROWS, 1)
     t.useBuiltinScene(hippt.SCENE_SPHERE4)
-    for k, v in ((hippt.OPT_WAVE_THRESHOLD, -1), (hippt.OPT_SCRATCH_MB, 32768), (hippt.OPT_CHUNK, 256),
+    for k, v in ((hippt.OPT_WAVE_THRESHOLD, -1), (hippt.OPT_SCRATCH_MB, 32768), (hippt.OPT_CHUNK, 0),
                  (hippt.OPT_COUNT_TRAVERSAL, 0), (hippt.OPT_BLOCKS_PER_CU, 0), (hippt.OPT_LDS_SCENE, 1),
                  (hippt.OPT_PATH_MODE, 0), (hippt.OPT_WAVEFRONT_SLOTS, 1 << 24), (hippt.OPT_LEAF_EXIT, -1),
                  (hippt.OPT_NODE_EXIT, -1), (hippt.OPT_BVH_SAH, 1), (hippt.OPT_BVH_WIDTH, 0),
@@ -724,6 +724,25 @@ def test_chained_batches_camera_change_and_row_shares(pt):
         share = pt.readback()
         rows = np.arange(r, h, 4)
         _assert_same(share[0][rows], share[1][rows], full[0][rows], full[1][rows])
+    pt.setRowRange(0, 0)
+
+
+def test_automatic_chain_and_claim_size(pt):
+    """HIPPT_OPT_CHAIN -1 and HIPPT_OPT_CHUNK 0 (the defaults) as applied (HIPPT_INFO_CHAIN_CAP,
+    HIPPT_INFO_CHUNK): a whole 1080p/64 spp Cornell batch runs unchained with 512-item claims; its 1/8
+    row share chains 8 batches with 256-item claims; blob70k's whole image (a tree in global memory)
+    chains 3."""
+    lib = hippt.load_library()
+    pt.setOption(hippt.OPT_CHAIN, -1)
+    pt.setOption(hippt.OPT_CHUNK, 0)
+    for name, stride, cap, chunk in (("cornell34", 1, 0, 512), ("cornell34", 8, 8, 256), ("blob70k", 1, 3, 512)):
+        pt.uploadMesh(scenes.get_scene(name))
+        pt.setRowInterleave(0, stride)
+        assert pt.initialize(1920, 1080)
+        assert lib.hipptRenderFramesAsync(0, 64, 8, None)
+        assert pt.synchronize()
+        assert lib.hipptGetOption(hippt.INFO_CHAIN_CAP) == cap, name
+        assert lib.hipptGetOption(hippt.INFO_CHUNK) == chunk, name
     pt.setRowRange(0, 0)
 
 
