@@ -1090,6 +1090,8 @@ def test_bench_json_contract():
     r = d["roofline"]
     assert r["bound"] == "valu" and r["unit"] == "TFLOP/s" and r["achieved"] > 0 and r["peak"] == 157.3
     assert abs(r["frac"] - r["achieved"] / r["peak"]) < 1e-3
-    assert r["algorithmic_bytes"]["per_launch"] > 0
+    # per step (a chained launch may trace several steps, another none): kernel time, FLOP and bytes
+    assert r["algorithmic_bytes"]["per_step"] > 0 and r["kernel_ms_per_step"] > 0 and r["launches_per_step"] > 0
+    assert d["config"]["chunk"]["applied"] in (256, 512) and "applied_cap" in d["config"]["chain"]
     cb = d["cpu_baseline"]
     assert cb["kind"] == "port" and cb["value"] > 0 and cb["cores"] >= 1 and cb["unit"] == "Msamples/s"
