@@ -2,10 +2,10 @@
 """Summarise a tools/profile.sh run into profiles/<tag>_summary.md and profiles/pmc_summary.json.
 
 Launch order of bench.py: a counted pass (mesh_kernel<true>), then the warmup steps and the timed
-steps (mesh_kernel<false>, one launch enqueued per step; with chained batches some launches trace
-several steps and others only combine).  rocprofv3 -T truncates the template instances to
-"mesh_kernel", so the timed launches are the last `steps` mesh_kernel dispatches; every figure is
-per STEP (their sum / steps), not per launch.
+steps (mesh_kernel<false>; with chained batches a launch may trace several steps, another only
+combine, and a step may have no launch of its own).  rocprofv3 -T truncates the template instances
+to "mesh_kernel", so the timed launches are the last launches_per_step x steps mesh_kernel
+dispatches (the bench line's count); every figure is per STEP (their sum / steps), not per launch.
 
 HBM bytes follow MI355X_MICROARCH.md §HBM with this kernel's own access widths calibrated on a known
 byte count (tools/micro/pmc_bytes.hip, profiles/round5/pmc_bytes_factors.json): FETCH_SIZE and
@@ -37,8 +37,9 @@ def dispatches(path, name="mesh_kernel"):
     return rows
 
 
-def counters(path, last):
-    """Per-step sums of each counter over the last `last` mesh_kernel dispatches (the timed steps)."""
+def counters(path, last, steps):
+    """Per-step sums of each counter over the last `last` mesh_kernel dispatches (the timed launches of
+    `steps` steps)."""
     per = defaultdict(dict)
     for r in csv.DictReader(open(path)):
         if not r["Kernel_Name"].startswith("mesh_kernel"):
@@ -49,7 +50,7 @@ def counters(path, last):
     for i in ids:
         for k, v in per[i].items():
             out[k] += v
-    return {k: v / last for k, v in out.items()}, len(ids)
+    return {k: v / steps for k, v in out.items()}, len(ids)
 
 
 FACTORS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles", "round5",
@@ -89,15 +90,18 @@ def main():
     repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     bench = load_json_line(os.path.join(root, "kt_bench.json"))
     steps = bench["steps"]
+    # the timed launches: one per step, or fewer with chained batches (a step posted before the run's
+    # last launch started has none; bench.py's launches_per_step counts them)
+    launches = int(round(bench["roofline"].get("launches_per_step", 1.0) * steps))
     kt = dispatches(os.path.join(root, "kt", "run_kernel_trace.csv"))
-    timed = kt[-steps:]
+    timed = kt[-launches:]
     durs = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in timed]
     mean_ms = sum(durs) / steps  # kernel time per step
     c = {}
     for sub in ("pmc_fetch", "pmc_write", "pmc_sq", "pmc_sq2", "pmc_ta"):
         p = os.path.join(root, sub, "run_counter_collection.csv")
         if os.path.exists(p):
-            vals, n = counters(p, steps)
+            vals, n = counters(p, launches, steps)
             c.update(vals)
     cfg = bench["config"]
     f_fetch, f_write, model = traffic_model(cfg["scene"])
