@@ -545,7 +545,8 @@ def main():
                 "chain": {"option": pt._lib.hipptGetOption(hippt.OPT_CHAIN),
                           "applied_cap": pt._lib.hipptGetOption(hippt.INFO_CHAIN_CAP),
                           "note": "HIPPT_OPT_CHAIN (default -1, automatic: chained for batches of at most "
-                                  "2^26 samples and for trees in global memory): a launch whose batch is "
+                                  "2^26 samples, trees in global memory and the general kernel): a launch "
+                                  "whose batch is "
                                   "drained goes on with the steps posted behind it (ring of batches, "
                                   "hippt_trace.h), a later launch combines them, and a step posted before "
                                   "the run's last launch has started gets no launch of its own; every "

@@ -253,9 +253,9 @@ enum {
                                        many (1..8), so that the run pays the launch's tail once per that many
                                        batches; the next launch combines them beside its own paths and the
                                        image's readers flush the rest.  0: one launch per batch; -1
-                                       (default): automatic (on for batches of at most 2^26 samples and for
-                                       trees in global memory, 2..8 batches by the batch's size).  Same
-                                       results either way */
+                                       (default): automatic (on for batches of at most 2^26 samples, for
+                                       trees in global memory and for the general kernel; 2..8 batches by
+                                       the batch's size).  Same results either way */
 };
 /* Output frame word formats (HIPPT_OPT_PIXEL_FORMAT).  Both map an accumulated colour c to
  * sqrt(clamp(c, 0, 1)) per channel.

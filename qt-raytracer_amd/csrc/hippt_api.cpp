@@ -1052,13 +1052,14 @@ bool batch_scratch(Ctx &c, size_t need, float **out, const char **err) {
 // a whole 1080p/64 spp image, 8 of its 1/4 and 1/8 row shares); the ring holds twice that, so that a
 // launch traces one group of batches while it combines the previous one.
 // Automatic (HIPPT_OPT_CHAIN -1): chained batches for every batch of at most 2^26 samples (the row
-// shares of a 1080p/64 spp image split over 2 or more GPUs) and for trees in global memory; a whole
-// image of an LDS-resident scene runs one launch per batch.  Measured (r5s, 20 steps, cap by
-// chain_cap): 1/8 shares Cornell 1.112 -> 1.047 ms, blob70k 3.003 -> 2.518, cornell_mixed 1.831 ->
-// 1.573; 1/2 shares blob70k 9.79 -> 9.49, cornell_mixed 6.20 -> 5.92, Cornell 3.757 -> 3.765; whole
-// images blob70k 18.94 -> 18.69, but Cornell 7.255 -> 7.321: a whole Cornell batch has little tail to
+// shares of a 1080p/64 spp image split over 2 or more GPUs), for trees in global memory and for the
+// general kernel (spheres, Metal/Dielectric); a whole image of an LDS-resident Lambertian scene runs
+// one launch per batch.  Measured (r5s/r5x, 20 steps, cap by chain_cap): 1/8 shares Cornell 1.112 ->
+// 1.047 ms, blob70k 3.003 -> 2.518, cornell_mixed 1.831 -> 1.573; 1/2 shares blob70k 9.79 -> 9.49,
+// cornell_mixed 6.20 -> 5.92, Cornell 3.757 -> 3.765; whole images blob70k 18.94 -> 18.69,
+// cornell_mixed 12.06 -> 11.70, but Cornell 7.255 -> 7.321: a whole Cornell batch has little tail to
 // save, and a run pays its first launch's start and its last group's combine without overlap.
-bool chain_auto(unsigned total, bool ldsScene) { return total <= (1u << 26) || !ldsScene; }
+bool chain_auto(unsigned total, bool ldsScene, bool full) { return total <= (1u << 26) || !ldsScene || full; }
 // chain_batch's launch skip (an A/B build knob)
 #ifndef HIPPT_CHAIN_SKIP
 #define HIPPT_CHAIN_SKIP 1
@@ -1392,7 +1393,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                     const bool fuse = maxDepth > 0 && s.pathMode == 0 && s.fuseCombine != 0;
                     // chained batches (Ctx::chain): asynchronous camera-pool megakernel batches over
                     // 4-wide float nodes whose items fit the ring's slot bits
-                    const bool chained = fuse && !copy && !cnt && (s.chainBatches > 0 || (s.chainBatches < 0 && chain_auto(total, ldsScene))) &&
+                    const bool chained = fuse && !copy && !cnt && (s.chainBatches > 0 || (s.chainBatches < 0 && chain_auto(total, ldsScene, s.scene.full))) &&
                                          poolWords != 0 &&
                                          fmt == hippt::kWideFloat && c.meshBlocksPerCuChain > 0 &&
                                          total <= (1u << hippt::kChainMaxShift);
