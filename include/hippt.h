@@ -184,8 +184,9 @@ enum {
                                        16 for LDS-resident scenes, 32 otherwise */
     HIPPT_OPT_SCRATCH_MB = 3,       /* cap of the per-batch sample scratch per device (32768: one batch for 4K x 256 spp) */
     HIPPT_OPT_CHUNK = 4,            /* work items a wave takes from the global queue at once (64..2^20, a
-                                       multiple of 64); 0 (default): automatic, 512 for whole-image batches
-                                       (>= 2^26 samples) of the Lambertian megakernel, else 256 */
+                                       multiple of 64); 0 (default): automatic, 512 for chained or
+                                       whole-image (>= 2^26 samples) batches of the Lambertian megakernel,
+                                       else 256 */
     HIPPT_OPT_BLOCKS_PER_CU = 5,    /* persistent-grid residency (0 = occupancy query) */
     HIPPT_OPT_LDS_SCENE = 6,        /* 1 (default): small scenes are copied into LDS per block */
     HIPPT_OPT_PATH_MODE = 8,        /* 0 (default): persistent megakernel; 1: wavefront kernels */

@@ -1442,13 +1442,15 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         // +5.8% over 32 with the exits below, r6c)
                         const bool fullMega = s.pathMode == 0 && s.scene.full;
                         p.waveThreshold = s.waveThreshold >= 0 ? s.waveThreshold : ldsScene || fullMega ? 24 : 32;
-                        // claim size: 512 items for whole-image batches of the Lambertian kernels
-                        // (Cornell 1080p/64 spp 7.255 -> 7.199 ms, blob70k 18.94 -> 18.91, r5s); 256
-                        // for smaller batches (1/8 shares: Cornell 1.112 -> 1.137 and blob70k 3.00 ->
-                        // 3.22 with 512) and the general kernel (cornell_mixed 12.06 -> 12.22)
-                        p.chunk = s.chunk > 0                                                   ? s.chunk
-                                  : s.pathMode == 0 && !s.scene.full && total >= (1u << 26) ? 512u
-                                                                                             : 256u;
+                        // claim size: 512 items for the Lambertian kernels' chained and whole-image
+                        // batches (Cornell 1080p/64 spp 7.255 -> 7.199 ms, blob70k 18.94 -> 18.91,
+                        // r5s; chained 1/8 shares Cornell 1.062 -> 1.041, blob70k 2.546 -> 2.547,
+                        // r5ab); 256 for small unchained batches (1/8 shares: Cornell 1.112 -> 1.137
+                        // and blob70k 3.00 -> 3.22 with 512) and the general kernel (cornell_mixed
+                        // 12.06 -> 12.22)
+                        p.chunk = s.chunk > 0 ? s.chunk
+                                  : s.pathMode == 0 && !s.scene.full && (chained || total >= (1u << 26)) ? 512u
+                                                                                                         : 256u;
                         // Loop exits of the traversal round (measured): trees in global
                         // memory leave the node loop once <= 17 lanes still search for a leaf (r2
                         // sweep of the 4-wide kernels: blob70k, 21 levels, best at 17-18; blob64x34
