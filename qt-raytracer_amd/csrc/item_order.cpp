@@ -202,12 +202,27 @@ void build_item_table(const std::vector<float> &cost, unsigned bandPixels, unsig
         if (s1 == s0) continue;
         const size_t f0 = s0 / runs, f1 = (s1 - 1) / runs;
         size_t out = s0;
+#ifdef HIPPT_EXP_ORDER_CYCLES
+        // experiment: the queue's frames in HIPPT_EXP_ORDER_CYCLES consecutive parts, each walked
+        // longest first on its own (a big batch ordered like a chain of small ones)
+        const size_t parts = HIPPT_EXP_ORDER_CYCLES, nf = f1 - f0 + 1;
+        for (size_t c = 0; c < parts; ++c) {
+            const size_t fa = f0 + nf * c / parts, fb = f0 + nf * (c + 1) / parts;
+            for (size_t k = 0; k + 1 < group.size(); ++k)
+                for (size_t f = fa; f < fb; ++f)
+                    for (size_t q = group[k]; q < group[k + 1]; ++q) {
+                        const size_t sl = f * runs + ranked[q];
+                        if (sl >= s0 && sl < s1) table[out++] = item(sl);
+                    }
+        }
+#else
         for (size_t k = 0; k + 1 < group.size(); ++k)
             for (size_t f = f0; f <= f1; ++f)
                 for (size_t q = group[k]; q < group[k + 1]; ++q) {
                     const size_t sl = f * runs + ranked[q];
                     if (sl >= s0 && sl < s1) table[out++] = item(sl);
                 }
+#endif
         s0 = s1;
     }
     for (; s0 < slots; ++s0) table[s0] = item(s0);
