@@ -187,10 +187,9 @@ struct Ctx {
         hippt::MeshParams key{};  // what every batch of the run shares (chain_same)
         long long blocks = 0;
         unsigned lastOwn = 0;     // the batch of the run's last enqueued launch
-        // a batch posted without a launch of its own (chain_batch: the last enqueued launch had not
-        // started, so it takes the batch): its parameters, launched by flush_chain if the run ends
-        // before another launch (a launch of the run still to start then finds the run closed)
-        bool pend = false;
+        // batches held for one group launch while the run's last launch has not started (chain_batch):
+        // the first one's parameters and their count; flush_chain launches them if the run ends first
+        unsigned pendN = 0;
         hippt::MeshParams pendP{};
     } chain;
     hipEvent_t chainStartEv = nullptr;  // recorded before each chained launch (chain_batch's skip test)
@@ -985,13 +984,12 @@ bool flush_chain(Ctx &c, const char **err) {
     Ctx::Chain &ch = c.chain;
     if (!ch.live) return true;
     HIP_TRY(hipSetDevice(c.device));
-    if (ch.pend) {
-        // before the run closes: the launch its batches since the last launch would have had, from the
-        // first of them through the last posted (the last launch, yet to start, may find the run closed)
+    if (ch.pendN) {  // the held batches' group launch, before the run closes
+        ch.pendP.chainGroup = ch.pendN;
         ch.pendP.chainPosted = ch.seq - 1u;
 #ifdef HIPPT_CHAIN_TRACE
-        std::fprintf(stderr, "chain run %u catch-up own %u posted %u epoch %u\n", ch.run, ch.pendP.chainSeq,
-                     ch.pendP.chainPosted, ch.epoch);
+        std::fprintf(stderr, "chain run %u group at close: own %u batches %u epoch %u\n", ch.run,
+                     ch.pendP.chainSeq, ch.pendN, ch.epoch);
 #endif
         if (!launch_chained(c, ch.pendP, err)) return false;
     }
@@ -1060,7 +1058,7 @@ bool batch_scratch(Ctx &c, size_t need, float **out, const char **err) {
 // cornell_mixed 12.06 -> 11.70, but Cornell 7.255 -> 7.321: a whole Cornell batch has little tail to
 // save, and a run pays its first launch's start and its last group's combine without overlap.
 bool chain_auto(unsigned total, bool ldsScene, bool full) { return total <= (1u << 26) || !ldsScene || full; }
-// chain_batch's launch skip (an A/B build knob)
+// chain_batch's held groups (an A/B build knob)
 #ifndef HIPPT_CHAIN_SKIP
 #define HIPPT_CHAIN_SKIP 1
 #endif
@@ -1103,7 +1101,7 @@ bool launch_chained(Ctx &c, hippt::MeshParams &p, const char **err) {
     Ctx::Chain &ch = c.chain;
     p.chainEpoch = ch.epoch++;
     ch.lastOwn = p.chainSeq;
-    ch.pend = false;
+    ch.pendN = 0;
     if (!c.chainStartEv) HIP_TRY(hipEventCreateWithFlags(&c.chainStartEv, hipEventDisableTiming));
     EventPair ev;
     if (!next_events(c, ev, err)) return false;
@@ -1116,15 +1114,15 @@ bool launch_chained(Ctx &c, hippt::MeshParams &p, const char **err) {
 }
 
 // Makes batch `p` (its parameters otherwise complete, `blocks` its grid) the next batch of the open
-// run, or of a new run (the old one flushed first): the chain fields, the ring slot's scratch, the
-// mailbox post, and the launch.  The launch is skipped when the run's last enqueued launch has not
-// started yet and may trace this batch (within chainCap of its own): posted before that launch
-// starts, the batch is normally taken by it (a wave leaves a run only at the launch's last batch or
-// at a batch not yet posted), so the launch it would have had could only combine.  Without the skip,
-// a burst of async batches leaves one such combine-only launch per batch behind each tracing launch
-// (~21 us each, plus the gap between launches; r5j).  The next launch of the run (or the run's
-// catch-up launch in flush_chain) starts at the first skipped batch, so a skipped batch the last
-// launch did not take is traced there.
+// run, or of a new run (the old one flushed first): the chain fields, the ring slot's scratch, and
+// the launch.  While the run's last enqueued launch has not started, batches are held (not posted)
+// and then launched together as one group (MeshParams::chainGroup, up to chainCap): the group is one
+// job whose queues walk the item order once for all its batches, as one batch of that many frames
+// would (a chain of small batches walks it once per batch: -3.6% for a 1/8 share, r5ad), and a burst
+// of async batches gets one launch per group instead of one per batch (each a ~21 us launch that
+// finds its batch taken, plus the gap between launches; r5j).  A batch launched on its own is posted
+// in the mailbox, so that a running launch may go on with it (chained batches); held batches are
+// not, so no launch but their group's takes them.
 bool chain_batch(Ctx &c, hippt::MeshParams &p, long long blocks, long long option, const char **err) {
     Ctx::Chain &ch = c.chain;
     p.comb = hippt::CombineParams{c.accum, c.out, nullptr, p.bandPixels, p.totalItems, 0, p.frames, p.comb.format};
@@ -1170,7 +1168,7 @@ bool chain_batch(Ctx &c, hippt::MeshParams &p, long long blocks, long long optio
         ch.seq = 0;
         ch.epoch = 0;
         ch.lastOwn = 0;
-        ch.pend = false;
+        ch.pendN = 0;
         ch.firstFrame = p.firstFrame;
         ch.step = -1;
         ch.slots = slots;
@@ -1195,34 +1193,32 @@ bool chain_batch(Ctx &c, hippt::MeshParams &p, long long blocks, long long optio
     p.chainCap = ch.cap;
     p.chainStep = ch.step;
     p.chainPosted = ch.seq;
-    // post: one word, so that a launch reads the run, its frame pattern and the last batch together
-    const unsigned long long consecutive = ch.step > 0 ? 1u : 0u;
-    __atomic_store_n(c.chainBox, ((unsigned long long)ch.run << 33) | (consecutive << 32) | ch.seq, __ATOMIC_RELEASE);
+    p.chainGroup = 1;
     c.hostSamples += p.totalItems;
-    // (the query after the post: a launch found not started reads the mailbox after it)
-    const bool skip = ch.epoch > 0 && ch.seq <= ch.lastOwn + ch.cap - 1u && kChainSkip &&
+    const unsigned seq = ch.seq++;
+    // held while the last launch has not started and the group is not full (64-item runs only: the
+    // group interleaves its batches' runs)
+    const bool hold = kChainSkip && ch.epoch > 0 && ch.pendN + 1u < ch.cap && p.totalItems % 64u == 0 &&
                       hipEventQuery(c.chainStartEv) == hipErrorNotReady;
 #ifdef HIPPT_CHAIN_TRACE
-    std::fprintf(stderr, "chain run %u seq %u %s (lastOwn %u epoch %u cap %u slots %u)\n", ch.run, ch.seq,
-                 skip ? "skipped" : "launched", ch.lastOwn, ch.epoch, ch.cap, ch.slots);
+    std::fprintf(stderr, "chain run %u seq %u %s (held %u epoch %u cap %u slots %u)\n", ch.run, seq,
+                 hold ? "held" : ch.pendN ? "launched with the held ones" : "launched", ch.pendN, ch.epoch,
+                 ch.cap, ch.slots);
 #endif
-    ++ch.seq;
-    if (skip) {
-        if (!ch.pend) {  // the run's first batch without a launch since its last launch
-            ch.pend = true;
-            ch.pendP = p;
-        }
+    if (hold) {
+        if (!ch.pendN) ch.pendP = p;
+        ++ch.pendN;
         return true;
     }
-    if (ch.pend) {
-        // The batches posted without a launch since the last one: this launch starts at the first of
-        // them (its own) and knows them all posted, so that it traces whatever the last launch did not
-        // take.  (The skip only expects the last launch to take them; the image never depends on it,
-        // nor on when the host saw that launch start.)
+    if (ch.pendN) {  // the held batches and this one: one group launch
         hippt::MeshParams q = ch.pendP;
-        q.chainPosted = p.chainSeq;
+        q.chainGroup = ch.pendN + 1u;
+        q.chainPosted = seq;
         return launch_chained(c, q, err);
     }
+    // post: one word, so that a launch reads the run, its frame pattern and the last batch together
+    const unsigned long long consecutive = ch.step > 0 ? 1u : 0u;
+    __atomic_store_n(c.chainBox, ((unsigned long long)ch.run << 33) | (consecutive << 32) | seq, __ATOMIC_RELEASE);
     return launch_chained(c, p, err);
 }
 

@@ -127,6 +127,10 @@ struct MeshParams {
     unsigned chainSlots, chainShift, chainCap;
     int chainStep;
     unsigned chainPosted;  // the run's last batch posted when the launch was enqueued (>= chainSeq)
+    // batches chainSeq .. chainSeq + chainGroup - 1 are this launch's own group, traced as one job: one
+    // set of queues over their items, each queue's cost order walked once for the whole group (64-item
+    // runs of the group's batches interleaved); 1: the own batch alone
+    unsigned chainGroup;
 };
 
 // Chained batches: the control block (unsigned words).  Ring slot k's block at k * kChainBlockWords:

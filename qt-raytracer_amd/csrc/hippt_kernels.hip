@@ -539,13 +539,22 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                         bool want = true;
                         for (;;) {
                             const unsigned t = __builtin_amdgcn_readfirstlane(cw->t);
+                            // the own group's queue (ChainWave::stat) spans its batches' items
+                            const bool grp = t == __builtin_amdgcn_readfirstlane(cw->stat);
+                            const unsigned nb = grp ? late_field(chainGroup) : 1u;
                             const unsigned got =
                                 queue_fetch(want, Q, chain_block(late_field(chainCtl), t, late_field(chainSlots)),
-                                            late_field(totalItems), late_field(chunk),
-                                            t == __builtin_amdgcn_readfirstlane(cw->stat), drained, t);
+                                            late_field(totalItems) * nb, late_field(chunk), grp, drained, t);
                             if (want && got != kNone) {
                                 raw = got;
                                 tItem = t;
+                                if (nb > 1u) {
+                                    // group position m: 64-item block m >> 6 is block (m >> 6) / nb of
+                                    // batch t + (m >> 6) % nb, so the group walks the one-batch order once
+                                    const unsigned blk = got >> 6, q = blk / nb;
+                                    raw = (q << 6) | (got & 63u);
+                                    tItem = t + (blk - q * nb);
+                                }
                                 want = false;
                             }
                             if (!__ballot(want) || !chain_next(Q, cw, view)) break;
@@ -899,6 +908,8 @@ hipError_t launch_mesh(const MeshParams &p, int blocks, bool countTraversal, hip
     if (chain && (!p.chainBox || p.chainSlots < 2 || p.chainSlots > kChainSlotsMax || (p.chainSlots & (p.chainSlots - 1)) ||
                   p.chainShift > kChainMaxShift || p.totalItems > (1u << p.chainShift) || p.chainCap < 1 ||
                   p.chainCap >= p.chainSlots || p.chainPosted < p.chainSeq || p.chainPosted - p.chainSeq >= p.chainCap ||
+                  p.chainGroup < 1 || p.chainGroup > p.chainCap || p.chainPosted - p.chainSeq + 1 < p.chainGroup ||
+                  (p.chainGroup > 1 && p.totalItems % 64u) ||
                   p.comb.bandPixels != p.bandPixels || p.comb.frames != p.frames))
         return hipErrorInvalidValue;
     const size_t bytes = mesh_lds_bytes(p.stackDepth, lds ? p.numNodes : 0, lds ? p.numTris : 0, p.wide != 0, p.topBytes,

@@ -467,7 +467,7 @@ __device__ __forceinline__ void chain_begin(WorkQueue &Q, ChainWave *cw, ChainVi
     unsigned *const ctl = late_field(chainCtl);
     const unsigned e = late_field(chainEpoch), own = late_field(chainSeq), R = late_field(chainSlots);
     const unsigned posted = late_field(chainPosted);
-    const unsigned total = late_field(totalItems), chunk = late_field(chunk);
+    const unsigned total = late_field(totalItems), chunk = late_field(chunk), group = late_field(chainGroup);
     // the first batch not combined by an earlier launch (written at the previous launch's start)
     const unsigned c0 = __builtin_amdgcn_readfirstlane(ctl[kChainCtlWord + 32u * ((e + 1u) & 1u)]);
     // lane k: batch t0 + k finished by an earlier launch (its slot's marker), within the ring's window
@@ -501,9 +501,11 @@ __device__ __forceinline__ void chain_begin(WorkQueue &Q, ChainWave *cw, ChainVi
             view->busy = 0;
         }
     }
-    if (u == own) {  // the own batch, untaken: first chunks static, as unchained
-        chain_mark(ctl, own, R, e);
-        queue_begin(Q, total, chunk);
+    if (u == own) {  // the own batch (group), untaken: first chunks static, as unchained
+        if (__lane_id() < group)
+            *reinterpret_cast<unsigned long long *>(chain_block(ctl, own + __lane_id(), R) + kChainMarkerWord) =
+                ((unsigned long long)(own + __lane_id()) << 32) | (e + 1u);
+        queue_begin(Q, total * group, chunk);
     } else {  // nothing to fetch: the wave's first refill moves it into batch u (chain_next)
         Q.left = 0;
         Q.next = Q.end = 0;
@@ -598,7 +600,9 @@ __device__ __forceinline__ void chain_ask(unsigned nt, ChainView *view, unsigned
 // the mailbox shows it posted (whole wave; at a camera-pool refill, so that the lanes whose paths
 // ended take the next batch's items while the others go on with theirs).
 __device__ __forceinline__ bool chain_next(WorkQueue &Q, ChainWave *cw, ChainView *view) {
-    const unsigned nt = __builtin_amdgcn_readfirstlane(cw->t) + 1u;
+    // (the own group's queue, ChainWave::stat, is followed by the batch after the group)
+    const unsigned t = __builtin_amdgcn_readfirstlane(cw->t);
+    const unsigned nt = t == __builtin_amdgcn_readfirstlane(cw->stat) ? t + late_field(chainGroup) : t + 1u;
     if (nt > __builtin_amdgcn_readfirstlane(cw->tLim)) return false;
     int step = int(__builtin_amdgcn_readfirstlane(unsigned(cw->step)));
     if (nt >= __builtin_amdgcn_readfirstlane(cw->posted)) {

@@ -1,0 +1,30 @@
+# round 5: held batches launched as one group (MeshParams::chainGroup) — parity (chain_debug
+# sequences with the decision trace, the chained GPU subset), then A/B against the previous library
+set -o pipefail
+cd /tmp
+export TMPDIR=/tmp
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+O=gpurun_out/r5ae
+mkdir -p $O
+HIPPT_LIB=qt-raytracer_amd/libv_trace.so timeout -k 10 200 python -u tools/exp/chain_debug3.py 1 > $O/dbg3.txt 2> $O/dbg3.err || { tail -20 $O/dbg3.err; exit 1; }
+grep -v " 0 px differ, 0 NaN" $O/dbg3.txt; grep -c "0 px differ, 0 NaN" $O/dbg3.txt
+timeout -k 10 200 python -u tools/exp/chain_debug.py cornell34 > $O/dbg_cornell.txt 2>&1 || { cat $O/dbg_cornell.txt; exit 1; }
+grep -c " 0 px differ" $O/dbg_cornell.txt
+timeout -k 10 500 python -u -m pytest tests/test_gpu_parity.py tests/test_gpu_headline.py -x -v --timeout 200 --timeout-method thread -k "chained or deferred_combine or async or pool or skipped or automatic" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+run() {  # name lib scene ranks opts...
+  local name=$1 lib=$2 sc=$3 r=$4; shift 4
+  HIPPT_LIB=qt-raytracer_amd/$lib.so timeout -k 10 100 python -u tools/band_scaling.py --scene $sc --steps 20 --ranks $r "$@" > $O/$name.jsonl || exit 1
+  echo "$name $(cat $O/$name.jsonl)"
+}
+for pass in 1 2; do
+  for lib in libhippt libv_prev; do
+    run p${pass}_${lib}_cornell_share $lib cornell34 8 28=1
+    run p${pass}_${lib}_cornell_quarter $lib cornell34 4 28=1
+    run p${pass}_${lib}_blob_share $lib blob70k 8 28=1
+    run p${pass}_${lib}_blob_whole $lib blob70k 1 28=1
+    run p${pass}_${lib}_mixed_whole $lib cornell_mixed 1 28=1
+  done
+done
+timeout -k 10 120 rocprofv3 --kernel-trace --stats -T --output-format csv -d $O/kt_share -o run -- \
+    python3 tools/band_scaling.py --scene cornell34 --steps 20 --ranks 8 28=1 > /dev/null 2>&1 || exit 1
