@@ -548,8 +548,8 @@ def main():
                                   "2^26 samples, trees in global memory and the general kernel): a launch "
                                   "whose batch is "
                                   "drained goes on with the steps posted behind it (ring of batches, "
-                                  "hippt_trace.h), a later launch combines them, and a step posted before "
-                                  "the run's last launch has started gets no launch of its own; every "
+                                  "hippt_trace.h), a later launch combines them, and steps that arrive before "
+                                  "the run's last launch has started are launched together as one group; every "
                                   "step's frames are traced and combined inside the timed region"},
                 "item_order": {"option": 1, "library_default": -1,
                                "note": "run-cost estimate computed on the first (counted, untimed) call, "
