@@ -1059,10 +1059,10 @@ bool batch_scratch(Ctx &c, size_t need, float **out, const char **err) {
 // save, and a run pays its first launch's start and its last group's combine without overlap.
 bool chain_auto(unsigned total, bool ldsScene, bool full) { return total <= (1u << 26) || !ldsScene || full; }
 // chain_batch's held groups (an A/B build knob)
-#ifndef HIPPT_CHAIN_SKIP
-#define HIPPT_CHAIN_SKIP 1
+#ifndef HIPPT_CHAIN_GROUPS
+#define HIPPT_CHAIN_GROUPS 1
 #endif
-constexpr bool kChainSkip = HIPPT_CHAIN_SKIP != 0;
+constexpr bool kChainGroups = HIPPT_CHAIN_GROUPS != 0;
 
 unsigned chain_cap(long long option, unsigned total) {
     if (option > 0) return unsigned(std::min<long long>(option, 8));
@@ -1198,7 +1198,7 @@ bool chain_batch(Ctx &c, hippt::MeshParams &p, long long blocks, long long optio
     const unsigned seq = ch.seq++;
     // held while the last launch has not started and the group is not full (64-item runs only: the
     // group interleaves its batches' runs)
-    const bool hold = kChainSkip && ch.epoch > 0 && ch.pendN + 1u < ch.cap && p.totalItems % 64u == 0 &&
+    const bool hold = kChainGroups && ch.epoch > 0 && ch.pendN + 1u < ch.cap && p.totalItems % 64u == 0 &&
                       hipEventQuery(c.chainStartEv) == hipErrorNotReady;
 #ifdef HIPPT_CHAIN_TRACE
     std::fprintf(stderr, "chain run %u seq %u %s (held %u epoch %u cap %u slots %u)\n", ch.run, seq,

@@ -365,10 +365,12 @@ __device__ __forceinline__ unsigned order_item_late(unsigned it) {
 }
 
 // ---- chained batches (MeshParams::chain*, CHAIN kernels) ----------------------------
-// One launch per asynchronous batch is still enqueued, but a launch whose batch is drained goes on with
-// the batches of its run the host has posted behind it, so that a run of batches pays the launch's
-// tail (the last paths finishing at falling lane use, ~0.2-0.3 ms) once per chainCap batches instead
-// of once per batch.  The rules that keep it exact:
+// A launch whose batch is drained goes on with the batches of its run the host has posted behind it,
+// so that a run of batches pays the launch's tail (the last paths finishing at falling lane use,
+// ~0.2-0.3 ms) once per chainCap batches instead of once per batch; batches that arrive while the
+// run's last launch has not started are held on the host and launched as one group
+// (MeshParams::chainGroup: the launch's own batches, one set of queues over their items).  The rules
+// that keep it exact:
 //  * a launch starts after the previous one on the stream has ended, so every batch before its own
 //    is finished, and so is every batch an earlier launch moved into (a wave leaves a batch only once
 //    all of its queues are drained, and a launch ends only when its waves have finished their paths):
@@ -377,10 +379,11 @@ __device__ __forceinline__ unsigned order_item_late(unsigned it) {
 //    yet combined, [c0, c1], beside its own tracing (the fused combine of one batch before), and
 //    records c1 + 1 for the next launch (by epoch parity: the next launch reads it, this one's late
 //    waves do not see it);
-//  * it traces from u = c1 + 1 (its own batch when no earlier launch took it: the first chunks then
-//    static, as unchained) up to min(c0 + slots - 1, u + chainCap - 1), so that it never writes a ring
-//    slot it combines or one a batch not yet combined holds; the host posts a batch in the mailbox
-//    before its launch is enqueued, and a launch takes a later batch only once the mailbox shows it;
+//  * it traces from u = c1 + 1 (its own batch or group when no earlier launch took it: the first
+//    chunks then static, as unchained) up to min(c0 + slots - 1, u + chainCap - 1), so that it never
+//    writes a ring slot it combines or one a batch not yet combined holds; the host posts a batch
+//    launched on its own in the mailbox before its launch is enqueued, never a held one, and a launch
+//    takes a later batch only once the mailbox shows it;
 //  * the counters of the slots it combines are zeroed at its start for the batches that reuse them
 //    (no wave of the launch reads them: it traces only past c1);
 //  * the run's last combines are the final flush (launch_chain_flush), before anything reads or
@@ -393,7 +396,7 @@ struct ChainWave {
     unsigned posted;    // batches before this one are known posted
     int step;           // frames from one batch to the next (-1: not known yet)
     unsigned c0, c1;    // this launch's combine range (c1 < c0: none)
-    unsigned stat;      // the batch whose queues have static first chunks (~0u: none)
+    unsigned stat;      // the own batch (group) whose queues have static first chunks (~0u: none)
 };
 
 // The block's view of the mailbox (in its first wave's WaveWords; chain_next): batches up to `last`
