@@ -748,11 +748,13 @@ def test_automatic_chain_and_claim_size(pt):
 
 
 def test_chained_batches_with_skipped_launches(pt):
-    """chain_batch posts a batch without a launch of its own while the run's last launch has not
-    started (that launch takes it); a run that closes with such batches (a camera change, a readback)
-    gets one catch-up launch.  Batches long enough (256 frames of 96x54) that each launch is still
-    queued behind the running one when the next batches are posted: the images equal one launch per
-    batch, before and after a camera change, and the sample count is exact."""
+    """chain_batch holds the batches that arrive while the run's last launch has not started and
+    launches them together as one group (MeshParams::chainGroup: one set of queues over the group's
+    items, 64-item runs of its batches interleaved); a run that closes with held batches (a camera
+    change, a readback) launches them first.  Batches long enough (256 frames of 96x54) that each
+    launch is still queued behind the running one when the next batches arrive: the images equal one
+    launch per batch, before and after a camera change, at caps 8 and 3, and the sample count is
+    exact."""
     import ctypes
     sc = scenes.cornell34()
     w, h = 96, 54
