@@ -423,11 +423,7 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
     ChainWave *const cw = &ww->cw;
     WaveWords *const bw = reinterpret_cast<WaveWords *>(reinterpret_cast<char *>(lds) + P.poolOffset);
     ChainView *const view = &bw->view;
-#ifdef HIPPT_EXP_NODRAINED
-    unsigned *const drained = POOL && CHAIN ? bw->drained : nullptr;
-#else
     unsigned *const drained = POOL ? bw->drained : nullptr;  // the block's drained-queue words
-#endif
     // CHAIN kernels keep the work queue and the segment count in LDS (ww->Q, ww->segs), the others in
     // registers
     WorkQueue Q;
@@ -653,12 +649,10 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
         // ---- shading: lanes whose traversal finished (ray_color step, RayTracer.h:579-596) ----
         // (a lane resuming a pending draw continues its segment; CHAIN kernels count the wave's
         // segments in ww->segs, one LDS add per round)
-#ifndef HIPPT_EXP_CHAIN_NOSEGS
         if constexpr (CHAIN) {
             const unsigned long long sm = __ballot(item != kNone && !busy(T) && !(CAP && pend != 0u));
             if (__lane_id() == 0 && sm) atomicAdd(&ww->segs, unsigned(__popcll(sm)));
         }
-#endif
         if (item != kNone && !busy(T)) {
             prof<STATS>(pc, 6);
             const bool cont = CAP && pend != 0u;  // resumes a pending draw: same segment

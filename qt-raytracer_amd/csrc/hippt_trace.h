@@ -167,24 +167,15 @@ __device__ __forceinline__ void queue_select(WorkQueue &Q, unsigned g, unsigned 
     Q.g = g;
     Q.qEnd = queue_start(total, g + 1);
     Q.waves = 4u * ((gridDim.x + kQueues - 1 - g) / kQueues);  // blocks b = g mod 8, 4 waves each
-#ifdef HIPPT_EXP_NO_STATIC
-    Q.dynBase = queue_start(total, g);
-#else
     Q.dynBase = queue_start(total, g) + Q.waves * chunk;
-#endif
 }
 
 __device__ __forceinline__ void queue_begin(WorkQueue &Q, unsigned total, unsigned chunk) {
     queue_select(Q, blockIdx.x % kQueues, total, chunk);
     Q.left = kQueues;
     const unsigned wid = (blockIdx.x / kQueues) * 4u + (threadIdx.x >> 6);
-#ifdef HIPPT_EXP_NO_STATIC
-    (void)wid;
-    Q.next = Q.end = 0;
-#else
     Q.next = min(queue_start(total, Q.g) + wid * chunk, Q.qEnd);
     Q.end = min(Q.next + chunk, Q.qEnd);
-#endif
 }
 
 // A queue found drained, for the block (LDS word drained[t & 1] = t << 8 | one bit per queue of
@@ -664,14 +655,7 @@ __device__ __forceinline__ void camera_sample(const PP &P, unsigned it, Ray &r, 
 // cost three, and the store instructions of lanes finishing at different times dominated the
 // address unit's load on LDS-resident scenes).
 __device__ __forceinline__ void store_radiance(float *scratch, unsigned item, float r, float g, float b) {
-#ifdef HIPPT_EXP_NT_RADIANCE
-    float *const d = scratch + 3 * size_t(item);
-    __builtin_nontemporal_store(r, d);
-    __builtin_nontemporal_store(g, d + 1);
-    __builtin_nontemporal_store(b, d + 2);
-#else
     *reinterpret_cast<float3 *>(scratch + 3 * size_t(item)) = make_float3(r, g, b);
-#endif
 }
 
 // Sky gradient on a miss (RayTracer.h:593-595), times throughput; `inv` = 1/sqrtf(|d|^2).
