@@ -257,7 +257,24 @@ enum {
                                        (default): automatic (on for batches of at most 2^26 samples, for
                                        trees in global memory and for the general kernel; 2..8 batches by
                                        the batch's size).  Same results either way */
+    , HIPPT_OPT_CHAIN_AUDIT = 31    /* 1: chained launches record, per batch of each run, the work items they
+                                       traced (count and a hash of their indices), the frames and the launch
+                                       they traced them with, and the pixels, frames and launch of the batch's
+                                       combine; read with hipptChainAudit.  0 (default): off.  Takes effect at
+                                       the next run.  Same images either way (a testing aid) */
 };
+/* Records of the chained runs closed since the last call (HIPPT_OPT_CHAIN_AUDIT), as 32-bit words:
+ * per run a 16-word header  [0] 0xC4A1D17 [1] run id [2] device [3] batch 0's first frame [4] frames
+ * from one batch to the next (-1: one batch) [5] frames per batch [6] band pixels [7] items per batch
+ * [8] batches [9] launches [10] slots [11] batches beyond the records (their records pooled in the
+ * last one) [12..15] 0, then min(batches, 256) + 1 records of 16 words: [0] items traced [1] pixels
+ * combined [2..3] sum of hash(item) [4..5] sum of hash(pixel) over the combine (64-bit, mod 2^64;
+ * hash(i) = the RNG hash of i ^ 0x5bd1e995) [6] 1 + largest first frame an item was traced with
+ * [7] ~smallest [8] 1 + latest launch that traced items [9] ~earliest [10] 1 + latest launch that
+ * combined pixels (the run's last flush is launch `launches`) [11] ~earliest [12] 1 + largest first
+ * frame the combine used [13] ~smallest [14..15] 0.  Writes at most maxWords words (whole runs) and
+ * returns the number written; runs that did not fit are kept for the next call.  Synchronises. */
+int hipptChainAudit(unsigned int *words, int maxWords);
 /* Output frame word formats (HIPPT_OPT_PIXEL_FORMAT).  Both map an accumulated colour c to
  * sqrt(clamp(c, 0, 1)) per channel.
  *   ARGB:  0xAARRGGBB, channel = uint(x * 255) truncated (CudaPathTracerKernel.cu:171-178).

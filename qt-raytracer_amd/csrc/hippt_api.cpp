@@ -191,7 +191,18 @@ struct Ctx {
         // the first one's parameters and their count; flush_chain launches them if the run ends first
         unsigned pendN = 0;
         hippt::MeshParams pendP{};
+        unsigned *audit = nullptr;  // the run's audit records (HIPPT_OPT_CHAIN_AUDIT), or null
     } chain;
+    // HIPPT_OPT_CHAIN_AUDIT: kAuditRuns runs' records on the device (run k in slab k % kAuditRuns) and
+    // the headers of the runs not yet copied to the host (State::auditWords), oldest first
+    unsigned *auditDev = nullptr;
+    unsigned auditNext = 0;
+    struct AuditRun {
+        unsigned hdr[hippt::kAuditWords];
+        unsigned slab;
+        bool closed;
+    };
+    std::vector<AuditRun> auditRuns;
     hipEvent_t chainStartEv = nullptr;  // recorded before each chained launch (chain_batch's skip test)
     unsigned *chainCtl = nullptr;
     float *chainScratch = nullptr;
@@ -266,6 +277,8 @@ struct State {
     int fuseCombine = -1;  // combine inside the next megakernel launch (HIPPT_OPT_FUSE_COMBINE)
     int itemOrder = -1;    // scene-hitting pixel runs first (HIPPT_OPT_ITEM_ORDER; -1: automatic)
     int chainBatches = -1; // batches a chained launch may trace (HIPPT_OPT_CHAIN; 0 off, -1 automatic)
+    bool chainAudit = false;            // HIPPT_OPT_CHAIN_AUDIT
+    std::vector<unsigned> auditWords;   // closed runs' audit words not yet read (hipptChainAudit)
     std::vector<std::pair<int, uint32_t *>> rngTables;  // per device, built on first use
     unsigned activeTopBytes = 0;  // of the last mesh render (hipptGetOption HIPPT_INFO_*)
     int activeBlocksPerCu = 0;
@@ -366,6 +379,12 @@ void build_camera(const double lookfrom[3], const double lookat[3], const double
     out.reserved = 0.0f;
 }
 
+// The held batches of the open chain run (Ctx::chain.pendN) launched now as one group: before
+// anything frees or replaces a buffer their parameters (Ctx::chain.pendP) point at — scene buffers,
+// node layouts, item tables, the spill area (a held group launched after the free read
+// freed memory).  The run stays open.
+bool launch_held(Ctx &c, const char **err);
+
 // Item tables no launch reads any more are freed; with `all`, after waiting for the stream.
 void free_retired_tables(Ctx &c, bool all) {
     size_t k = 0;
@@ -422,9 +441,13 @@ void free_scene_buffers(Ctx &c) {
     c.sceneVersion = -1;
 }
 
+void harvest_audit(Ctx &c);
+
 void destroy_ctx(Ctx &c) {
     (void)hipSetDevice(c.device);
     if (c.stream) (void)hipStreamSynchronize(c.stream);
+    harvest_audit(c);  // closed runs' records; an open run's (its image discarded) are dropped
+    (void)hipFree(c.auditDev);
     (void)hipFree(c.accum);
     (void)hipFree(c.out);
     (void)hipFree(c.scratch);
@@ -524,6 +547,9 @@ bool harvest_locked(Ctx &c, const char **err) {
 bool ensure_scene(Ctx &c, const char **err) {
     State &s = S();
     if (s.scene.kind != HIPPT_SCENE_MESH || c.sceneVersion == s.scene.version) return true;
+    if (!launch_held(c, err)) return false;
+    HIP_TRY(hipSetDevice(c.device));
+    HIP_TRY(hipStreamSynchronize(c.stream));  // queued launches read the old buffers
     free_scene_buffers(c);
     auto up = [&](float4 *&dst, const std::vector<float4> &src) -> bool {
         HIP_TRY(hipMalloc(&dst, std::max<size_t>(16, src.size() * sizeof(float4))));
@@ -623,6 +649,7 @@ bool ensure_order(Ctx &c, const CameraF &cam, int frames, int maxDepth, bool for
             }
             return true;  // this batch in image order
         }
+        if (!launch_held(c, err)) return false;
         for (auto &t : c.orderTables) retire_table(c, t.dev);
         c.orderTables.clear();
         c.runCosts = std::move(cost);
@@ -648,6 +675,7 @@ bool ensure_order(Ctx &c, const CameraF &cam, int frames, int maxDepth, bool for
         return fail(err, "HIP path tracer: item table upload failed");
     }
     if (c.orderTables.size() >= kOrderTables) {
+        if (!launch_held(c, err)) return false;
         retire_table(c, c.orderTables.back().dev);
         c.orderTables.pop_back();
     }
@@ -677,6 +705,7 @@ bool ensure_half(Ctx &c, const char **err) {
     SceneHost &sc = S().scene;
     if (!half_tree_ok(sc)) return fail(err, "HIP path tracer: no half-precision tree for this scene");
     if (c.halfVersion == sc.version && c.nodes4f) return true;
+    if (!launch_held(c, err)) return false;
     HIP_TRY(hipSetDevice(c.device));
     HIP_TRY(hipStreamSynchronize(c.stream));
     (void)hipFree(c.nodes4f);
@@ -700,6 +729,7 @@ bool ensure_hybrid(Ctx &c, int top, const char **err) {
         sc.hybridTop = top;
     }
     if (c.hybridTop == top && c.nodes4h) return true;
+    if (!launch_held(c, err)) return false;
     HIP_TRY(hipSetDevice(c.device));
     HIP_TRY(hipStreamSynchronize(c.stream));
     (void)hipFree(c.nodes4h);
@@ -792,6 +822,7 @@ bool ensure_spill(Ctx &c, hippt::MeshParams &p, long long blocks, bool spills, i
     p.spillCap = spillCap;
     const size_t bytes = size_t(blocks) * hippt::kMeshBlock * size_t(spillCap) * sizeof(int);
     if (c.spillBytes < bytes) {
+        if (!launch_held(c, err)) return false;
         HIP_TRY(hipStreamSynchronize(c.stream));
         (void)hipFree(c.spill);
         c.spill = nullptr;
@@ -984,15 +1015,7 @@ bool flush_chain(Ctx &c, const char **err) {
     Ctx::Chain &ch = c.chain;
     if (!ch.live) return true;
     HIP_TRY(hipSetDevice(c.device));
-    if (ch.pendN) {  // the held batches' group launch, before the run closes
-        ch.pendP.chainGroup = ch.pendN;
-        ch.pendP.chainPosted = ch.seq - 1u;
-#ifdef HIPPT_CHAIN_TRACE
-        std::fprintf(stderr, "chain run %u group at close: own %u batches %u epoch %u\n", ch.run,
-                     ch.pendP.chainSeq, ch.pendN, ch.epoch);
-#endif
-        if (!launch_chained(c, ch.pendP, err)) return false;
-    }
+    if (!launch_held(c, err)) return false;  // the held batches' group launch, before the run closes
     ch.live = false;
     hippt::ChainFlushParams f{};
     f.comb = ch.key.comb;
@@ -1003,6 +1026,15 @@ bool flush_chain(Ctx &c, const char **err) {
     f.slots = ch.slots;
     f.shift = ch.shift;
     f.step = std::max(ch.step, 0);
+    f.audit = ch.audit;
+    if (ch.audit && !c.auditRuns.empty()) {  // the run's header: what it asked for
+        Ctx::AuditRun &a = c.auditRuns.back();
+        a.hdr[4] = unsigned(ch.step);
+        a.hdr[8] = ch.seq;
+        a.hdr[9] = ch.epoch;
+        a.hdr[11] = ch.seq > hippt::kAuditBatches ? ch.seq - hippt::kAuditBatches : 0u;
+        a.closed = true;
+    }
     EventPair ev;
     if (!next_events(c, ev, err)) return false;
     HIP_TRY(hipEventRecord(ev.a, c.stream));
@@ -1070,6 +1102,64 @@ unsigned chain_cap(long long option, unsigned total) {
     return unsigned(std::clamp(c, 2.0, 8.0));
 }
 
+// The ring of a run of `total`-item batches: 2^shift samples per slot (the slot bits above them in
+// an item), at least 2 x cap slots (a launch traces up to cap batches while up to cap batches before
+// its own wait for its combine), 12 bytes per sample.  The ring stays within the sample-scratch
+// budget (HIPPT_OPT_SCRATCH_MB): the cap shrinks until it fits, and a batch whose smallest ring
+// (2 slots) does not fit runs unchained (bytes = 0).  (blob70k at 1080p/64 spp and cap 8
+// asked for 25.8 GB whatever the budget.)
+struct RingPlan {
+    unsigned cap = 0, slots = 0, shift = 0;
+    size_t bytes = 0;
+};
+RingPlan ring_plan(unsigned total, long long option, size_t budget) {
+    RingPlan r;
+    r.shift = 6;
+    while ((1u << r.shift) < total) ++r.shift;
+    const size_t slotBytes = (size_t(1) << r.shift) * 3 * sizeof(float);
+    for (unsigned cap = chain_cap(option, total); cap >= 1; --cap) {
+        unsigned slots = 2;
+        while (slots < 2 * cap) slots <<= 1;
+        slots = std::min(slots, hippt::kChainSlotsMax);
+        if (size_t(slots) * slotBytes <= budget) {
+            r.cap = cap;
+            r.slots = slots;
+            r.bytes = size_t(slots) * slotBytes;
+            return r;
+        }
+    }
+    return r;
+}
+
+// The ring's buffers for plan `r` (allocated, or grown after the open run's last combines); *ok =
+// false when the device has no memory for them (the batch then runs unchained).
+bool ensure_ring(Ctx &c, const RingPlan &r, bool *ok, const char **err) {
+    *ok = true;
+    if (!c.chainCtl) HIP_TRY(hipMalloc(&c.chainCtl, hippt::kChainCtlWords * sizeof(unsigned)));
+    if (!c.chainBox) {
+        HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c.chainBox), sizeof(unsigned long long),
+                              hipHostMallocMapped | hipHostMallocCoherent));
+        *c.chainBox = 0;
+        void *d = nullptr;
+        HIP_TRY(hipHostGetDevicePointer(&d, c.chainBox, 0));
+        c.chainBoxDev = static_cast<unsigned long long *>(d);
+    }
+    if (c.chainScratchBytes >= r.bytes) return true;
+    if (!flush_deferred(c, err)) return false;  // the open run's last combines read the old ring
+    HIP_TRY(hipStreamSynchronize(c.stream));
+    (void)hipFree(c.chainScratch);
+    c.chainScratch = nullptr;
+    c.chainScratchBytes = 0;
+    if (hipMalloc(&c.chainScratch, r.bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        c.chainScratch = nullptr;
+        *ok = false;
+        return true;
+    }
+    c.chainScratchBytes = r.bytes;
+    return true;
+}
+
 bool same_cam(const CameraF &a, const CameraF &b) {
     if (a.lens_radius != b.lens_radius) return false;
     for (int k = 0; k < 3; ++k)
@@ -1113,6 +1203,43 @@ bool launch_chained(Ctx &c, hippt::MeshParams &p, const char **err) {
     return true;
 }
 
+bool launch_held(Ctx &c, const char **err) {
+    Ctx::Chain &ch = c.chain;
+    if (!ch.live || !ch.pendN) return true;
+    HIP_TRY(hipSetDevice(c.device));
+    ch.pendP.chainGroup = ch.pendN;
+    ch.pendP.chainPosted = ch.seq - 1u;
+#ifdef HIPPT_CHAIN_TRACE
+    std::fprintf(stderr, "chain run %u group launched early: own %u batches %u epoch %u\n", ch.run, ch.pendP.chainSeq,
+                 ch.pendN, ch.epoch);
+#endif
+    return launch_chained(c, ch.pendP, err);
+}
+
+// The closed runs' audit records to State::auditWords (the context's stream finished past their
+// final flush: after a synchronisation).  A run still open stays.
+void harvest_audit(Ctx &c) {
+    if (!c.auditDev) return;
+    State &s = S();
+    size_t k = 0;
+    for (auto &a : c.auditRuns) {
+        if (!a.closed) {
+            c.auditRuns[k++] = a;
+            continue;
+        }
+        const unsigned recs = std::min(a.hdr[8], hippt::kAuditBatches) + 1u;
+        std::vector<unsigned> w(size_t(recs) * hippt::kAuditWords);
+        if (hipMemcpy(w.data(), c.auditDev + size_t(a.slab) * hippt::kAuditRunWords, w.size() * sizeof(unsigned),
+                      hipMemcpyDeviceToHost) != hipSuccess) {
+            (void)hipGetLastError();
+            continue;
+        }
+        s.auditWords.insert(s.auditWords.end(), a.hdr, a.hdr + hippt::kAuditWords);
+        s.auditWords.insert(s.auditWords.end(), w.begin(), w.end());
+    }
+    c.auditRuns.resize(k);
+}
+
 // Makes batch `p` (its parameters otherwise complete, `blocks` its grid) the next batch of the open
 // run, or of a new run (the old one flushed first): the chain fields, the ring slot's scratch, and
 // the launch.  While the run's last enqueued launch has not started, batches are held (not posted)
@@ -1123,7 +1250,7 @@ bool launch_chained(Ctx &c, hippt::MeshParams &p, const char **err) {
 // finds its batch taken, plus the gap between launches; r5j).  A batch launched on its own is posted
 // in the mailbox, so that a running launch may go on with it (chained batches); held batches are
 // not, so no launch but their group's takes them.
-bool chain_batch(Ctx &c, hippt::MeshParams &p, long long blocks, long long option, const char **err) {
+bool chain_batch(Ctx &c, hippt::MeshParams &p, long long blocks, const RingPlan &ring, const char **err) {
     Ctx::Chain &ch = c.chain;
     p.comb = hippt::CombineParams{c.accum, c.out, nullptr, p.bandPixels, p.totalItems, 0, p.frames, p.comb.format};
     bool same = ch.live && blocks == ch.blocks && chain_same(p, ch.key);
@@ -1138,30 +1265,8 @@ bool chain_batch(Ctx &c, hippt::MeshParams &p, long long blocks, long long optio
     }
     if (!same) {
         if (!flush_deferred(c, err)) return false;  // the old run's (or an unchained batch's) combines
-        unsigned shift = 6;
-        while ((1u << shift) < p.totalItems) ++shift;
-        const unsigned cap = chain_cap(option, p.totalItems);
-        unsigned slots = 2;
-        while (slots < 2 * cap) slots <<= 1;
-        slots = std::min(slots, hippt::kChainSlotsMax);
-        const size_t bytes = (size_t(slots) << shift) * 3 * sizeof(float);
-        if (!c.chainCtl) HIP_TRY(hipMalloc(&c.chainCtl, hippt::kChainCtlWords * sizeof(unsigned)));
-        if (!c.chainBox) {
-            HIP_TRY(hipHostMalloc(reinterpret_cast<void **>(&c.chainBox), sizeof(unsigned long long),
-                                  hipHostMallocMapped | hipHostMallocCoherent));
-            *c.chainBox = 0;
-            void *d = nullptr;
-            HIP_TRY(hipHostGetDevicePointer(&d, c.chainBox, 0));
-            c.chainBoxDev = static_cast<unsigned long long *>(d);
-        }
-        if (c.chainScratchBytes < bytes) {
-            HIP_TRY(hipStreamSynchronize(c.stream));
-            (void)hipFree(c.chainScratch);
-            c.chainScratch = nullptr;
-            c.chainScratchBytes = 0;
-            HIP_TRY(hipMalloc(&c.chainScratch, bytes));
-            c.chainScratchBytes = bytes;
-        }
+        // (the ring's buffers: ensure_ring, before the batch was chained)
+        const unsigned shift = ring.shift, cap = ring.cap, slots = ring.slots;
         HIP_TRY(hipMemsetAsync(c.chainCtl, 0, hippt::kChainCtlWords * sizeof(unsigned), c.stream));
         ch.live = true;
         ch.run = (ch.run + 1u) & 0x7fffffffu;
@@ -1178,7 +1283,34 @@ bool chain_batch(Ctx &c, hippt::MeshParams &p, long long blocks, long long optio
         p.comb.scratch = c.chainScratch;
         p.comb.firstFrame = p.firstFrame;
         ch.key = p;
+        ch.audit = nullptr;
+        if (S().chainAudit) {
+            if (!c.auditDev) {
+                HIP_TRY(hipMalloc(&c.auditDev, size_t(hippt::kAuditRuns) * hippt::kAuditRunWords * sizeof(unsigned)));
+            }
+            if (c.auditRuns.size() >= hippt::kAuditRuns) {  // every slab holds a closed run: to the host first
+                HIP_TRY(hipStreamSynchronize(c.stream));
+                harvest_audit(c);
+            }
+            const unsigned slab = c.auditNext++ % hippt::kAuditRuns;
+            ch.audit = c.auditDev + size_t(slab) * hippt::kAuditRunWords;
+            HIP_TRY(hipMemsetAsync(ch.audit, 0, hippt::kAuditRunWords * sizeof(unsigned), c.stream));
+            Ctx::AuditRun a{};
+            a.hdr[0] = 0xC4A1D17u;
+            a.hdr[1] = ch.run;
+            a.hdr[2] = unsigned(c.device);
+            a.hdr[3] = unsigned(p.firstFrame);
+            a.hdr[4] = ~0u;
+            a.hdr[5] = unsigned(p.frames);
+            a.hdr[6] = p.bandPixels;
+            a.hdr[7] = p.totalItems;
+            a.hdr[10] = ch.slots;
+            a.slab = slab;
+            a.closed = false;
+            c.auditRuns.push_back(a);
+        }
     }
+    p.chainAudit = ch.audit;
     p.scratch = c.chainScratch;
     p.queue = c.chainCtl;
     p.combCtr = nullptr;
@@ -1389,10 +1521,17 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                     const bool fuse = maxDepth > 0 && s.pathMode == 0 && s.fuseCombine != 0;
                     // chained batches (Ctx::chain): asynchronous camera-pool megakernel batches over
                     // 4-wide float nodes whose items fit the ring's slot bits
-                    const bool chained = fuse && !copy && !cnt && (s.chainBatches > 0 || (s.chainBatches < 0 && chain_auto(total, ldsScene, s.scene.full))) &&
-                                         poolWords != 0 &&
-                                         fmt == hippt::kWideFloat && c.meshBlocksPerCuChain > 0 &&
-                                         total <= (1u << hippt::kChainMaxShift);
+                    bool chained = fuse && !copy && !cnt && (s.chainBatches > 0 || (s.chainBatches < 0 && chain_auto(total, ldsScene, s.scene.full))) &&
+                                   poolWords != 0 &&
+                                   fmt == hippt::kWideFloat && c.meshBlocksPerCuChain > 0 &&
+                                   total <= (1u << hippt::kChainMaxShift);
+                    RingPlan ring;
+                    if (chained) {
+                        ring = ring_plan(total, s.chainBatches, cap);
+                        bool ok = ring.bytes != 0;
+                        if (ok && !ensure_ring(c, ring, &ok, err)) return false;
+                        chained = ok;
+                    }
                     if ((!fuse || !chained) && !flush_chain(c, err)) return false;
                     if (!fuse && !flush_deferred(c, err)) return false;
                     float *scratch = nullptr;
@@ -1497,7 +1636,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                             s.activeChainCap = 0;
                             if (chained) {
                                 p.comb.format = s.pixelFormat;
-                                if (!chain_batch(c, p, blocks, s.chainBatches, err)) return false;
+                                if (!chain_batch(c, p, blocks, ring, err)) return false;
                                 s.activeChainCap = int(c.chain.cap);
                                 continue;  // launched or taken by the run's last launch; its combine
                                            // belongs to the run (Ctx::chain)
@@ -1549,6 +1688,7 @@ bool sync_locked(const char **err) {
         for (auto &pe : c.pending)
             if (!account(pe, c, err)) return false;
         c.pending.clear();
+        harvest_audit(c);
     }
     return true;
 }
@@ -2250,6 +2390,10 @@ extern "C" bool hipptSetOption(int key, long long value) try {
         if (value < -1 || value > 8) return false;
         s.chainBatches = int(value);
         return true;
+    case HIPPT_OPT_CHAIN_AUDIT:
+        if (value != 0 && value != 1) return false;
+        s.chainAudit = value == 1;
+        return true;
     default: return false;
     }
 } catch (const std::exception &e) {
@@ -2300,12 +2444,34 @@ extern "C" long long hipptGetOption(int key) try {
     case HIPPT_OPT_ITEM_ORDER: return s.itemOrder;
     case HIPPT_OPT_WAVEFRONT_SORT: return s.wfSort;
     case HIPPT_OPT_CHAIN: return s.chainBatches;
+    case HIPPT_OPT_CHAIN_AUDIT: return s.chainAudit ? 1 : 0;
     case HIPPT_INFO_LDS_TOP_BYTES: return s.activeTopBytes;
     case HIPPT_INFO_BLOCKS_PER_CU: return s.activeBlocksPerCu;
     case HIPPT_INFO_CHUNK: return s.activeChunk;
     case HIPPT_INFO_CHAIN_CAP: return s.activeChainCap;
     default: return -1;
     }
+} catch (const std::exception &e) {
+    return -1;
+} catch (...) {
+    return -1;
+}
+
+extern "C" int hipptChainAudit(unsigned int *words, int maxWords) try {
+    std::lock_guard<std::mutex> g(S().mu);
+    State &s = S();
+    const char *e = nullptr;
+    if (s.ready && !sync_locked(&e)) return -1;  // closes the open runs (their final flushes) first
+    size_t n = 0;
+    while (n < s.auditWords.size()) {
+        const size_t recs = std::min(s.auditWords[n + 8], hippt::kAuditBatches) + 1u;
+        const size_t len = (1 + recs) * hippt::kAuditWords;
+        if (n + len > size_t(std::max(0, maxWords))) break;
+        n += len;
+    }
+    if (words && n) std::memcpy(words, s.auditWords.data(), n * sizeof(unsigned));
+    s.auditWords.erase(s.auditWords.begin(), s.auditWords.begin() + long(n));
+    return int(n);
 } catch (const std::exception &e) {
     return -1;
 } catch (...) {

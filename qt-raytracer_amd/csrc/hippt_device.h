@@ -131,6 +131,9 @@ struct MeshParams {
     // set of queues over their items, each queue's cost order walked once for the whole group (64-item
     // runs of the group's batches interleaved); 1: the own batch alone
     unsigned chainGroup;
+    // HIPPT_OPT_CHAIN_AUDIT: the run's audit records (kAuditBatches + 1 records of kAuditWords words:
+    // per batch what was traced and combined, hipptChainAudit), or null
+    unsigned *chainAudit;
 };
 
 // Chained batches: the control block (unsigned words).  Ring slot k's block at k * kChainBlockWords:
@@ -157,7 +160,14 @@ struct ChainFlushParams {
     const unsigned *ctl;
     unsigned epoch, lastSeq, slots, shift;
     int step;
+    unsigned *audit;  // MeshParams::chainAudit
 };
+
+// Chained-batch audit records (HIPPT_OPT_CHAIN_AUDIT, include/hippt.h hipptChainAudit): per run, one
+// record of kAuditWords words per batch below kAuditBatches and one pooled record for the rest;
+// kAuditRuns runs' records per context on the device.
+constexpr unsigned kAuditBatches = 256, kAuditWords = 16, kAuditRuns = 64;
+constexpr unsigned kAuditRunWords = (kAuditBatches + 1) * kAuditWords;
 
 
 // MeshParams::wide

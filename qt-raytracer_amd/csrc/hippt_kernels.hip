@@ -303,10 +303,15 @@ __device__ __forceinline__ bool combine_chunk_chain(const ChainWave *cw) {
     base = __builtin_amdgcn_readfirstlane(base);
     if (base >= bandPixels) return false;
     const unsigned p = base + __lane_id();
+    const int c0 = int(__builtin_amdgcn_readfirstlane(cw->c0)), c1 = int(__builtin_amdgcn_readfirstlane(cw->c1));
     if (p < bandPixels)
-        combine_pixel_chain<8>(late_field(comb), late_field(scratch), p, int(__builtin_amdgcn_readfirstlane(cw->c0)),
-                               int(__builtin_amdgcn_readfirstlane(cw->c1)), late_field(chainSlots),
+        combine_pixel_chain<8>(late_field(comb), late_field(scratch), p, c0, c1, late_field(chainSlots),
                                late_field(chainShift), max(0, late_field(chainStep)));
+    if (unsigned *const audit = late_field(chainAudit)) {
+        const bool v = p < bandPixels;
+        audit_combine(audit, c0, c1, unsigned(__popcll(__ballot(v))), wave_sum(v ? audit_hash(p) : 0ull), e,
+                      late_field(comb.firstFrame), max(0, late_field(chainStep)));
+    }
     return true;
 }
 
@@ -542,15 +547,8 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                                 queue_fetch(want, Q, chain_block(late_field(chainCtl), t, late_field(chainSlots)),
                                             late_field(totalItems) * nb, late_field(chunk), grp, drained, t);
                             if (want && got != kNone) {
-                                raw = got;
-                                tItem = t;
-                                if (nb > 1u) {
-                                    // group position m: 64-item block m >> 6 is block (m >> 6) / nb of
-                                    // batch t + (m >> 6) % nb, so the group walks the one-batch order once
-                                    const unsigned blk = got >> 6, q = blk / nb;
-                                    raw = (q << 6) | (got & 63u);
-                                    tItem = t + (blk - q * nb);
-                                }
+                                // a group position: the group walks the one-batch order once
+                                chain::group_item(got, t, nb, raw, tItem);
                                 want = false;
                             }
                             if (!__ballot(want) || !chain_next(Q, cw, view)) break;
@@ -560,8 +558,11 @@ __global__ __launch_bounds__(kMeshBlock, (FULL || WIDE) ? HIPPT_WIDE_WAVES_PER_E
                         if (it != kNone) {
                             // the item's frames: its batch's offset from the launch's own batch's
                             const int step = int(__builtin_amdgcn_readfirstlane(unsigned(cw->step)));
-                            camera_sample(cam_args_late(), it, c, crng,
-                                          (tItem - late_field(chainSeq)) * unsigned(max(step, 0)));
+                            const unsigned fAdd = chain::frame_add(tItem, late_field(chainSeq), step);
+                            camera_sample(cam_args_late(), it, c, crng, fAdd);
+                            if (unsigned *const audit = late_field(chainAudit))
+                                audit_trace(audit, tItem, it, unsigned(late_field(firstFrame)) + fAdd,
+                                            late_field(chainEpoch));
                             it |= (tItem & (late_field(chainSlots) - 1u)) << late_field(chainShift);
                         }
                     } else {
@@ -759,8 +760,15 @@ __global__ __launch_bounds__(256) void chain_flush_kernel(ChainFlushParams P) {
     const int c1 = int(P.lastSeq);
     if (c1 < c0) return;
     const unsigned stride = gridDim.x * 256u;
-    for (unsigned p = blockIdx.x * 256u + threadIdx.x; p < P.comb.bandPixels; p += stride)
-        combine_pixel_chain<8>(P.comb, P.scratch, p, c0, c1, P.slots, P.shift, P.step);
+    // whole waves per step (the audit's wave sums)
+    for (unsigned base = blockIdx.x * 256u + (threadIdx.x & ~63u); base < P.comb.bandPixels; base += stride) {
+        const unsigned p = base + __lane_id();
+        const bool v = p < P.comb.bandPixels;
+        if (v) combine_pixel_chain<8>(P.comb, P.scratch, p, c0, c1, P.slots, P.shift, P.step);
+        if (P.audit)
+            audit_combine(P.audit, c0, c1, unsigned(__popcll(__ballot(v))), wave_sum(v ? audit_hash(p) : 0ull), P.epoch,
+                          P.comb.firstFrame, P.step);
+    }
 }
 
 // table[s] for s = 0 .. 2^32-1: the state from which random_in_unit_sphere, entered with state s,

@@ -10,6 +10,7 @@
 #pragma once
 
 #include "bvh_builder.h"
+#include "hippt_chain_logic.h"
 #include "hippt_device.h"
 
 #pragma clang fp contract(off)
@@ -444,8 +445,7 @@ __device__ __forceinline__ unsigned *chain_block(unsigned *ctl, unsigned t, unsi
 // Batch t taken by launch `epoch` (lane 0; every wave that moves into t stores the same word).
 __device__ __forceinline__ void chain_mark(unsigned *ctl, unsigned t, unsigned slots, unsigned epoch) {
     if (__lane_id() == 0)
-        *reinterpret_cast<unsigned long long *>(chain_block(ctl, t, slots) + kChainMarkerWord) =
-            ((unsigned long long)t << 32) | (epoch + 1u);
+        *reinterpret_cast<unsigned long long *>(chain_block(ctl, t, slots) + kChainMarkerWord) = chain::marker(t, epoch);
 }
 
 // queue_select for a batch with (stat) or without static first chunks
@@ -465,20 +465,17 @@ __device__ __forceinline__ void chain_begin(WorkQueue &Q, ChainWave *cw, ChainVi
     // the first batch not combined by an earlier launch (written at the previous launch's start)
     const unsigned c0 = __builtin_amdgcn_readfirstlane(ctl[kChainCtlWord + 32u * ((e + 1u) & 1u)]);
     // lane k: batch t0 + k finished by an earlier launch (its slot's marker), within the ring's window
-    const unsigned t0 = max(own, c0);
+    const unsigned t0 = chain::begin_t0(c0, own);
     bool fin = false;
-    if (__lane_id() < R && t0 + __lane_id() < c0 + R) {
+    if (chain::begin_lane_in_window(__lane_id(), t0, c0, R)) {
         const unsigned t = t0 + __lane_id();
-        const unsigned long long m =
-            *reinterpret_cast<const unsigned long long *>(chain_block(ctl, t, R) + kChainMarkerWord);
-        const unsigned by = unsigned(m);
-        fin = unsigned(m >> 32) == t && by != 0u && by <= e;
+        fin = chain::marker_finished(
+            *reinterpret_cast<const unsigned long long *>(chain_block(ctl, t, R) + kChainMarkerWord), t, e);
     }
     const unsigned nfin = unsigned(__builtin_ctzll(~__ballot(fin)));
-    // finished: every batch before the own one, and the run of marked batches from t0
-    const int c1 = max(int(t0 + nfin) - 1, int(own) - 1);
-    const unsigned u = unsigned(max(int(c0), c1 + 1));  // first batch to trace
-    const unsigned tLim = min(c0 + R - 1u, u + late_field(chainCap) - 1u);
+    const chain::BeginPlan plan = chain::begin_plan(c0, own, nfin, R, late_field(chainCap));
+    const int c1 = plan.c1;
+    const unsigned u = plan.u, tLim = plan.tLim;
     const int step = late_field(chainStep);
     if (__lane_id() == 0) {
         cw->c0 = c0;
@@ -490,7 +487,7 @@ __device__ __forceinline__ void chain_begin(WorkQueue &Q, ChainWave *cw, ChainVi
         cw->stat = u == own ? own : ~0u;
         if (threadIdx.x == 0) {
             view->last = posted;
-            view->flags = step > 0 ? 1u : 0u;
+            view->flags = chain::view_flags_at_start(step);
             view->stamp = 0;
             view->busy = 0;
         }
@@ -498,7 +495,7 @@ __device__ __forceinline__ void chain_begin(WorkQueue &Q, ChainWave *cw, ChainVi
     if (u == own) {  // the own batch (group), untaken: first chunks static, as unchained
         if (__lane_id() < group)
             *reinterpret_cast<unsigned long long *>(chain_block(ctl, own + __lane_id(), R) + kChainMarkerWord) =
-                ((unsigned long long)(own + __lane_id()) << 32) | (e + 1u);
+                chain::marker(own + __lane_id(), e);
         queue_begin(Q, total * group, chunk);
     } else {  // nothing to fetch: the wave's first refill moves it into batch u (chain_next)
         Q.left = 0;
@@ -509,7 +506,7 @@ __device__ __forceinline__ void chain_begin(WorkQueue &Q, ChainWave *cw, ChainVi
     // the work counters of the slots combined here (the counters of their next batches)
     if (blockIdx.x == 0 && threadIdx.x < 64u) {
         if (__lane_id() == 0) {
-            ctl[kChainCtlWord + 32u * (e & 1u)] = unsigned(max(int(c0), c1 + 1));
+            ctl[kChainCtlWord + 32u * (e & 1u)] = chain::begin_next_c0(c0, c1);
             ctl[kChainCtlWord + 64u + 32u * ((e + 1u) & 1u)] = 0u;
         }
         for (int b = int(c0); b <= c1; ++b)
@@ -528,12 +525,6 @@ __device__ __forceinline__ void chain_begin(WorkQueue &Q, ChainWave *cw, ChainVi
 // host word.  A querier that loses the claim sleeps (no memory traffic) for the winner's refresh,
 // then reads the copy once more.  Stale answers only ever say "not yet posted": a wave then stops
 // taking batches, and a later launch traces them.
-__device__ __forceinline__ void chain_copy_pack(unsigned long long now, unsigned long long h, unsigned run,
-                                                unsigned ep, unsigned long long &c) {
-    // the host on a later run: this one is closed (and the word's batch is that run's)
-    const bool closed = unsigned(h >> 33) != run;
-    c = ((now >> 4) << 40) | ((unsigned long long)ep << 34) | (closed ? (1ull << 33) : (h & ((1ull << 33) - 1ull)));
-}
 __device__ __forceinline__ void chain_ask(unsigned nt, ChainView *view, unsigned &last, unsigned &flags) {
     constexpr unsigned long long kBoxRefresh = 1000;  // 10 us of the 100 MHz clock
     constexpr unsigned kViewRefresh = 500, kWaitBusy = 20000;
@@ -543,7 +534,7 @@ __device__ __forceinline__ void chain_ask(unsigned nt, ChainView *view, unsigned
         flags = __hip_atomic_load(&view->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const unsigned st = __hip_atomic_load(&view->stamp, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         const unsigned now32 = unsigned(__builtin_amdgcn_s_memrealtime());
-        if (nt <= last || (flags & 2u) || (st != 0u && now32 - st < kViewRefresh)) return;
+        if (nt <= last || (flags & chain::kClosed) || (st != 0u && now32 - st < kViewRefresh)) return;
         unsigned idle = 0u;
         if (__hip_atomic_compare_exchange_strong(&view->busy, &idle, 1u, __ATOMIC_ACQUIRE, __ATOMIC_RELAXED,
                                                  __HIP_MEMORY_SCOPE_WORKGROUP))
@@ -556,33 +547,38 @@ __device__ __forceinline__ void chain_ask(unsigned nt, ChainView *view, unsigned
         flags = __hip_atomic_load(&view->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         return;
     }
+    // the view's only writer now (busy): merge into what it holds at this point, not into the words
+    // read before the claim, which another querier may have advanced since
+    last = __hip_atomic_load(&view->last, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    flags = __hip_atomic_load(&view->flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     unsigned long long *const box = reinterpret_cast<unsigned long long *>(late_field(chainCtl) + kChainBoxWord +
                                                                           (blockIdx.x % kQueues) * 32u);
     unsigned long long *const copy = box, *const claim = box + 1;
     const unsigned run = late_field(chainRun);
     // the copy and the claim carry the launch (epoch mod 64) that made them: a copy made by an earlier
     // launch says nothing about batches posted since, and chain_batch posts batches without a launch
-    // of their own only before the launch that is to take them starts (so its negative must be fresh)
+    // of their own only before the launch that is to take them starts (so its negative must be fresh).
+    // (A copy 64 launches old that looks fresh only says "not posted" or "open": view_merge never
+    // lowers what the view knows.)
     const unsigned ep = late_field(chainEpoch) & 63u;
     const unsigned long long now = __builtin_amdgcn_s_memrealtime();
     unsigned long long c = __hip_atomic_load(copy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const unsigned age = (unsigned(now >> 4) - unsigned(c >> 40)) & 0xffffffu;  // in 16-tick units
     const bool ours = (unsigned(c >> 34) & 63u) == ep;
-    if (unsigned(c) < nt && !((c >> 33) & 1ull) && (!ours || age >= kBoxRefresh / 16u)) {
+    if (chain::copy_last(c) < nt && !chain::copy_closed(c) && (!ours || age >= kBoxRefresh / 16u)) {
         const unsigned long long prev = __hip_atomic_load(claim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const bool active = (unsigned(prev) & 63u) == ep && now - (prev & ~63ull) < kBoxRefresh;
         if (!active && atomicCAS(claim, prev, (now & ~63ull) | ep) == prev) {  // this wave refreshes
             const unsigned long long h =
                 __hip_atomic_load(late_field(chainBox), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-            chain_copy_pack(__builtin_amdgcn_s_memrealtime(), h, run, ep, c);
+            c = chain::copy_pack(__builtin_amdgcn_s_memrealtime(), h, run, ep);
             __hip_atomic_store(copy, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {  // a refresh is in flight (claimed at most kBoxRefresh ago): give it 4 us, read once more
             while (__builtin_amdgcn_s_memrealtime() - now < 400u) __builtin_amdgcn_s_sleep(8);
             c = __hip_atomic_load(copy, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
-    last = max(last, unsigned(c));
-    flags = unsigned(c >> 32) & 3u;
+    chain::view_merge(last, flags, c);
     __hip_atomic_store(&view->flags, flags, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     __hip_atomic_store(&view->last, last, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
     __hip_atomic_store(&view->stamp, max(unsigned(__builtin_amdgcn_s_memrealtime()), 1u), __ATOMIC_RELAXED,
@@ -596,7 +592,7 @@ __device__ __forceinline__ void chain_ask(unsigned nt, ChainView *view, unsigned
 __device__ __forceinline__ bool chain_next(WorkQueue &Q, ChainWave *cw, ChainView *view) {
     // (the own group's queue, ChainWave::stat, is followed by the batch after the group)
     const unsigned t = __builtin_amdgcn_readfirstlane(cw->t);
-    const unsigned nt = t == __builtin_amdgcn_readfirstlane(cw->stat) ? t + late_field(chainGroup) : t + 1u;
+    const unsigned nt = chain::next_batch(t, __builtin_amdgcn_readfirstlane(cw->stat), late_field(chainGroup));
     if (nt > __builtin_amdgcn_readfirstlane(cw->tLim)) return false;
     int step = int(__builtin_amdgcn_readfirstlane(unsigned(cw->step)));
     if (nt >= __builtin_amdgcn_readfirstlane(cw->posted)) {
@@ -604,8 +600,8 @@ __device__ __forceinline__ bool chain_next(WorkQueue &Q, ChainWave *cw, ChainVie
         if (__lane_id() == 0) chain_ask(nt, view, last, flags);
         last = __builtin_amdgcn_readfirstlane(last);
         flags = __builtin_amdgcn_readfirstlane(flags);
-        if (nt > last) return false;  // not (yet) posted, or the run is closed
-        step = (flags & 1u) ? late_field(frames) : 0;
+        // not (yet) posted, the run closed before it, or its frame pattern not known here
+        if (!chain::view_takes(nt, last, flags, late_field(frames), step)) return false;
         if (__lane_id() == 0) {
             cw->posted = last + 1u;
             cw->step = step;
@@ -619,6 +615,43 @@ __device__ __forceinline__ bool chain_next(WorkQueue &Q, ChainWave *cw, ChainVie
     Q.left = kQueues;
     Q.next = Q.end = 0;
     return true;
+}
+
+// ---- chained-batch audit (MeshParams::chainAudit, HIPPT_OPT_CHAIN_AUDIT) --------------------------
+// Order-free summaries the host compares with what the run should have done (tests/chain_audit.py):
+// counts and 64-bit sums of a hash of the item / pixel indices, and min/max (as max of ~v) of the
+// frames and launches involved.
+__device__ __forceinline__ unsigned audit_hash(unsigned i) { return hash32(i ^ 0x5bd1e995u); }
+__device__ __forceinline__ unsigned *audit_record(unsigned *audit, unsigned t) {
+    return audit + min(t, kAuditBatches) * kAuditWords;
+}
+// one traced item (per lane, at the refill that generates its camera ray): its batch, index, the
+// first frame it was traced with and the launch.  Per-lane atomics: a wave-aggregated version costs
+// the chained kernels scratch spills in the refill (the audit is a testing aid; its atomics contend)
+__device__ __forceinline__ void audit_trace(unsigned *audit, unsigned t, unsigned item, unsigned frame,
+                                            unsigned epoch) {
+    unsigned *const r = audit_record(audit, t);
+    atomicAdd(r, 1u);
+    atomicAdd(reinterpret_cast<unsigned long long *>(r + 2), (unsigned long long)audit_hash(item));
+    atomicMax(r + 6, frame + 1u);
+    atomicMax(r + 7, ~frame);
+    atomicMax(r + 8, epoch + 1u);
+    atomicMax(r + 9, ~epoch);
+}
+// a wave's combine of `n` pixels (hash sum hsum) over batches [c0, c1] (lane 0)
+__device__ __forceinline__ void audit_combine(unsigned *audit, int c0, int c1, unsigned n, unsigned long long hsum,
+                                              unsigned epoch, int firstFrame, int step) {
+    if (__lane_id() != 0 || n == 0u) return;
+    for (int b = c0; b <= c1; ++b) {
+        unsigned *const r = audit_record(audit, unsigned(b));
+        const unsigned f0 = unsigned(firstFrame + b * step);
+        atomicAdd(r + 1, n);
+        atomicAdd(reinterpret_cast<unsigned long long *>(r + 4), hsum);
+        atomicMax(r + 10, epoch + 1u);
+        atomicMax(r + 11, ~epoch);
+        atomicMax(r + 12, f0 + 1u);
+        atomicMax(r + 13, ~f0);
+    }
 }
 
 // PP: MeshParams or CamArgs.  frameAdd: a chained batch's frame offset from the launch's own frames.

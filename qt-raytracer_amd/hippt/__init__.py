@@ -54,6 +54,7 @@ OPT_FUSE_COMBINE = 27
 OPT_ITEM_ORDER = 28
 OPT_WAVEFRONT_SORT = 29
 OPT_CHAIN = 30
+OPT_CHAIN_AUDIT = 31
 OPT_PIXEL_FORMAT = 25
 PIXEL_ARGB = 0
 PIXEL_RGBA8 = 1
@@ -75,7 +76,7 @@ EXPORTS = (
     "hipptGetOption",
     "hipptLastError", "hipptBvhBuild", "hipptBvhNodeCount", "hipptBvhDepth", "hipptBvhCopy", "hipptBvhFree",
     "hipptBvh4NodeCount", "hipptBvh4Depth", "hipptBvh4StackBound", "hipptBvh4Copy", "hipptBvh4QCopy", "hipptBvh4QNodeCount",
-    "hipptActiveBvhWidth",
+    "hipptActiveBvhWidth", "hipptChainAudit",
 )
 
 
@@ -186,6 +187,7 @@ def load_library(path: Optional[str] = None) -> ctypes.CDLL:
     sig("hipptBvh4Copy", None, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32))
     sig("hipptBvh4QCopy", None, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint32))
     sig("hipptBvh4QNodeCount", c_int, ctypes.c_void_p)
+    sig("hipptChainAudit", c_int, p_uint, c_int)
     _lib = lib
     return lib
 
@@ -461,6 +463,34 @@ class PathTracer:
 
     def resetStats(self) -> None:  # noqa: N802
         self._lib.hipptResetStats()
+
+
+AUDIT_MAGIC = 0xC4A1D17
+AUDIT_BATCHES = 256
+
+
+def chain_audit() -> list:
+    """The chained runs closed since the last call (HIPPT_OPT_CHAIN_AUDIT, include/hippt.h
+    hipptChainAudit): a list of (header dict, records uint32 array [batches + 1, 16]).  Synchronises."""
+    lib = load_library()
+    runs = []
+    while True:
+        buf = np.zeros(1 << 22, np.uint32)
+        n = lib.hipptChainAudit(_ptr(buf, ctypes.c_uint), buf.size)
+        if n < 0:
+            raise HipptError("hipptChainAudit failed")
+        if n == 0:
+            return runs
+        k = 0
+        while k < n:
+            h = buf[k:k + 16]
+            assert h[0] == AUDIT_MAGIC, "audit stream out of step"
+            hdr = dict(run=int(h[1]), device=int(h[2]), firstFrame=int(h[3].astype(np.int32)),
+                       step=int(h[4].astype(np.int32)), frames=int(h[5]), bandPixels=int(h[6]), totalItems=int(h[7]),
+                       batches=int(h[8]), launches=int(h[9]), slots=int(h[10]), overflow=int(h[11]))
+            recs = min(hdr["batches"], AUDIT_BATCHES) + 1
+            runs.append((hdr, buf[k + 16:k + 16 + recs * 16].reshape(recs, 16).copy()))
+            k += 16 + recs * 16
 
 
 def device_count() -> int:

@@ -1,0 +1,765 @@
+// chain_model.cpp — a host-compiled model of the chained-batch protocol (hippt_trace.h "chained
+// batches", hippt_api.cpp chain_batch / flush_chain), built and run by
+// tests/test_chain_protocol.py.  Test infrastructure, not product code.
+//
+// The integer rules come from the product's own header (qt-raytracer_amd/csrc/hippt_chain_logic.h:
+// view_merge, view_takes, begin_plan, marker_finished, next_batch, group_item, frame_add, copy_pack);
+// around them this file restates, as small state machines, what runs concurrently on the GPU and the
+// host: the waves of a launch (claiming work units from ring-slot counters, moving to the next batch,
+// asking the block's LDS view and the per-XCD copy of the mailbox in the same micro-steps as
+// chain_ask: two-word reads, the busy claim, the bounded wait, the refresh claim, the two-word
+// write), the combine of [c0, c1], the stream's order (launch, final flush, control-block reset),
+// and the host's chain_batch (new run, held batches, group launches, posting the mailbox word).
+// A seeded scheduler interleaves host calls and device micro-steps adversarially, with a clock that
+// makes views and copies fresh or stale at random.
+//
+// The anchor is the reference's accumulation: every frame's sample blended once, in frame order
+// (CudaPathTracerKernel.cu:157-178, 246-265).  Checked, per run and batch: every work unit traced
+// exactly once, with the batch's own frames; the ring slot holds that batch's radiance when it is
+// combined; every batch combined exactly once, in order, only after it is fully traced, with its own
+// frames; every wave of a launch computes the same plan; a wave's known step never changes.
+//
+// usage: chain_model fixed|legacy|small-ring|own-markers SEEDS [FIRST_SEED]   -> "violations N scenarios S ..." (exit 0)
+//        chain_model directed                          -> the GPUTEST_r05 interleaving, step by step
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <deque>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "hippt_chain_logic.h"
+
+using namespace hippt::chain;
+
+// ---- the rules under test ---------------------------------------------------------------------------
+struct Rules {
+    const char *name;
+    bool rereadAfterClaim;  // chain_ask merges into the view as it is after winning `busy`
+    void (*merge)(unsigned &, unsigned &, unsigned long long);
+    bool (*takes)(unsigned, unsigned, unsigned, int, int &);
+    unsigned (*startFlags)(int);
+};
+
+// Round 5's rules, restated (hippt_trace.h at 0c23542: chain_ask :584-586, chain_next :607-608,
+// chain_begin :493): the merge kept `last` but replaced the flags by the copy's (a closed copy
+// cleared the consecutive bit), merged into the words read before the claim, and a wave took any
+// batch <= last with step (flags & 1) ? frames : 0.
+static void legacy_view_merge(unsigned &last, unsigned &flags, unsigned long long c) {
+    if (unsigned(c) > last) last = unsigned(c);
+    flags = unsigned(c >> 32) & 3u;
+}
+static bool legacy_takes(unsigned nt, unsigned last, unsigned flags, int frames, int &step) {
+    if (nt > last) return false;
+    step = (flags & 1u) ? frames : 0;
+    return true;
+}
+static unsigned legacy_start_flags(int step) { return step > 0 ? 1u : 0u; }
+
+static const Rules kFixed{"fixed", true, view_merge, view_takes, view_flags_at_start};
+static const Rules kLegacy{"legacy", false, legacy_view_merge, legacy_takes, legacy_start_flags};
+
+// Mutants of the fixed rules (the model must catch each; tests/test_chain_protocol.py):
+// "small-ring": a ring of fewer than 2 x cap slots (chain_batch sizes it 2 x cap: a launch traces
+// up to cap batches while the batches before its own, up to cap of them, wait for its combine);
+// "own-markers": a launch counts the batches its own waves have moved into as finished.
+static const Rules kSmallRing{"small-ring", true, view_merge, view_takes, view_flags_at_start};
+static const Rules kOwnMarkers{"own-markers", true, view_merge, view_takes, view_flags_at_start};
+
+// ---- seeded randomness -------------------------------------------------------------------------------
+struct Rng {
+    uint64_t s;
+    explicit Rng(uint64_t seed) : s(seed * 0x9E3779B97F4A7C15ull + 0x1234567ull) {}
+    uint64_t next() {
+        s ^= s << 13;
+        s ^= s >> 7;
+        s ^= s << 17;
+        return s;
+    }
+    unsigned below(unsigned n) { return unsigned(next() % n); }
+    bool chance(double p) { return double(next() % 1000000) < p * 1e6; }
+};
+
+// device timing constants of chain_ask (100 MHz realtime ticks)
+constexpr unsigned long long kBoxRefresh = 1000;
+constexpr unsigned kViewRefresh = 500, kWaitBusy = 20000, kClaimWait = 400;
+
+struct Violations {
+    std::map<std::string, long> n;
+    std::string first;
+    void add(const std::string &kind, const std::string &what) {
+        if (n[kind]++ == 0 && first.empty()) first = kind + ": " + what;
+    }
+    long total() const {
+        long t = 0;
+        for (auto &kv : n) t += kv.second;
+        return t;
+    }
+};
+
+// ---- stream items ------------------------------------------------------------------------------------
+enum ItemKind { kLaunch, kFlush, kReset };
+struct Item {
+    ItemKind kind;
+    unsigned run = 0, own = 0, group = 1, posted = 0, epoch = 0, cap = 1, slots = 2, lastSeq = 0;
+    int step = -1, frames = 1, units = 1;
+    long ownFrame = 0;  // MeshParams::firstFrame of the own batch
+    long runFirst = 0;  // comb.firstFrame: batch 0's first frame
+    bool started = false;
+};
+
+struct Slot {  // ring slot radiance (one record per work unit)
+    bool valid = false;
+    unsigned run = 0, batch = 0;
+    long frame = 0;
+};
+
+struct Wave {
+    int block = 0;
+    enum Pc { kTrace, kNext, kAskTopLast, kAskTopFlags, kWait, kWaitLast, kWaitFlags, kClaimed, kCopyRead,
+              kRefresh, kClaimSleep, kMerge, kWriteFlags, kWriteLast, kRelease, kAnswer, kRetry, kPaths, kDone } pc = kTrace;
+    unsigned t = 0, stat = 0, tLim = 0, posted = 0;
+    int step = -1;
+    unsigned nt = 0, last = 0, flags = 0, askT0 = 0;
+    unsigned long long c = 0, until = 0;
+    bool closedTake = false;
+    unsigned want = 1;                                     // items the current refill still takes
+    std::vector<std::pair<unsigned, unsigned>> pending;  // (batch, unit) taken by the current refill
+    std::vector<std::pair<unsigned, unsigned>> pool;     // claimed, not yet handed to lanes
+};
+struct View {
+    unsigned last = 0, flags = 0, stamp = 0, busy = 0;
+};
+
+struct Model {
+    const Rules &R;
+    Rng rng;
+    Violations &V;
+    // configuration
+    unsigned cap, slots, blocks, wavesPerBlock, units, chunk;
+    double hostRate, retryRate, leaveRate;
+    // time
+    unsigned long long now = 1000000;
+    // host
+    unsigned long long box = 0;
+    struct HostRun {
+        bool live = false;
+        unsigned run = 0, seq = 0, epoch = 0, pendN = 0;
+        long firstFrame = 0;
+        int step = -1, frames = 1, key = 0;
+        Item pendP{kLaunch};
+        int lastLaunch = -1;  // stream index of the run's last enqueued launch
+    } H;
+    int key = 0;
+    long lastFF = 0;
+    // truth: frames of (run, batch) and what happened to them
+    std::map<std::pair<unsigned, unsigned>, long> truth;
+    std::map<std::pair<unsigned, unsigned>, std::vector<int>> traced;  // per unit: times traced
+    std::map<std::pair<unsigned, unsigned>, int> combined;
+    std::map<unsigned, long> nextCombine;  // per run: the batch its next combine must be
+    std::map<unsigned, unsigned> lastSeqOf;
+    // device
+    std::vector<Item> stream;
+    size_t head = 0;
+    std::vector<unsigned long long> markers;
+    std::vector<unsigned> counter;
+    unsigned cword[2] = {0, 0};
+    unsigned long long copy[8] = {}, claim[8] = {};
+    std::vector<std::vector<Slot>> scratch;
+    // the running launch
+    bool active = false;
+    std::vector<Wave> waves;
+    std::vector<View> views;
+    std::vector<bool> blockBegun;
+    bool planSet = false;
+    BeginPlan plan{};
+    unsigned planC0 = 0;
+    long combNext = 0;  // next batch of [c0, c1] the launch combines
+    unsigned gOwnLimit = 0;
+    long stats[4] = {0, 0, 0, 0};  // closed merges, answers from a closed view, takes from one
+
+    Model(const Rules &r, uint64_t seed, Violations &v) : R(r), rng(seed), V(v) {
+        cap = 1 + rng.below(8);
+        slots = 2;
+        while (slots < (&R == &kSmallRing ? cap : 2 * cap)) slots <<= 1;
+        if (slots > 16) slots = 16;
+        blocks = 1 + rng.below(4);
+        wavesPerBlock = 1 + rng.below(3);
+        units = 1 + rng.below(12);
+        const double rates[] = {0.02, 0.1, 0.3, 0.6};
+        hostRate = rates[rng.below(4)];
+        retryRate = rng.chance(0.5) ? 0.7 : 0.2;
+        const double leaves[] = {0.1, 0.4, 1.0};
+        leaveRate = leaves[rng.below(3)];
+        wavesPerBlock = 1 + rng.below(4);
+        chunk = 1u << rng.below(3);
+        markers.assign(16, 0);
+        counter.assign(16, 0);
+        scratch.assign(16, std::vector<Slot>(64));
+    }
+
+    std::string where() const {
+        char b[160];
+        std::snprintf(b, sizeof b, "cap %u slots %u blocks %u waves %u units %u hostRate %.2f", cap, slots, blocks,
+                      wavesPerBlock, units, hostRate);
+        return b;
+    }
+
+    // ---- host: chain_batch / flush_chain (hippt_api.cpp) ------------------------------------------
+    bool lastLaunchStarted() const { return H.lastLaunch < 0 || stream[size_t(H.lastLaunch)].started; }
+    void enqueueLaunch(Item p) {
+        p.epoch = H.epoch++;
+        H.pendN = 0;
+        stream.push_back(p);
+        H.lastLaunch = int(stream.size() - 1);
+    }
+    void flushChain() {
+        if (!H.live) return;
+        if (H.pendN) {
+            Item q = H.pendP;
+            q.group = H.pendN;
+            q.posted = H.seq - 1u;
+            enqueueLaunch(q);
+        }
+        H.live = false;
+        Item f{kFlush};
+        f.run = H.run;
+        f.epoch = H.epoch;
+        f.lastSeq = H.seq - 1u;
+        f.slots = slots;
+        f.step = H.step > 0 ? H.step : 0;
+        f.runFirst = H.firstFrame;
+        f.frames = H.frames;
+        f.units = int(units);
+        stream.push_back(f);
+        lastSeqOf[H.run] = H.seq - 1u;
+    }
+    void render(long ff, int frames, int k) {
+        bool same = H.live && H.key == k && H.frames == frames;
+        if (same && H.seq == 1) {
+            const long d = ff - H.firstFrame;
+            if (d == 0 || d == frames)
+                H.step = int(d);
+            else
+                same = false;
+        } else if (same && ff != H.firstFrame + long(H.seq) * H.step) {
+            same = false;
+        }
+        if (!same) {
+            flushChain();
+            stream.push_back(Item{kReset});
+            H.live = true;
+            H.run = (H.run + 1u) & 0x7fffffffu;
+            H.seq = H.epoch = H.pendN = 0;
+            H.firstFrame = ff;
+            H.step = -1;
+            H.frames = frames;
+            H.key = k;
+            H.lastLaunch = -1;
+            nextCombine[H.run] = 0;
+        }
+        Item p{kLaunch};
+        p.run = H.run;
+        p.own = H.seq;
+        p.posted = H.seq;
+        p.step = H.step;
+        p.cap = cap;
+        p.slots = slots;
+        p.frames = frames;
+        p.units = int(units);
+        p.ownFrame = ff;
+        p.runFirst = H.firstFrame;
+        truth[{H.run, H.seq}] = ff;
+        traced[{H.run, H.seq}] = std::vector<int>(units, 0);
+        const unsigned seq = H.seq++;
+        const bool hold = H.epoch > 0 && H.pendN + 1u < cap && !lastLaunchStarted();
+        if (hold) {
+            if (!H.pendN) H.pendP = p;
+            ++H.pendN;
+            return;
+        }
+        if (H.pendN) {
+            Item q = H.pendP;
+            q.group = H.pendN + 1u;
+            q.posted = seq;
+            enqueueLaunch(q);
+            return;
+        }
+        box = box_word(H.run, H.step > 0, seq);
+        enqueueLaunch(p);
+    }
+
+    void hostOp() {
+        // per scenario: how often the host leaves the run (burst of progressive batches, then a
+        // camera move) and how often it reads the image
+        unsigned r = rng.below(100);
+        if (r >= 55 && r < 92 && !rng.chance(leaveRate)) r = 0;
+        const int frames = H.live ? H.frames : 1 + int(rng.below(2));
+        if (r < 55) {
+            const long ff = H.live ? H.firstFrame + long(H.seq) * (H.step < 0 ? frames : H.step) : lastFF;
+            render(ff, frames, key);
+            lastFF = ff + frames;
+        } else if (r < 70) {
+            render(H.live ? H.firstFrame : lastFF, frames, key);  // the same frames again
+        } else if (r < 80) {
+            ++key;  // camera, scene, item order ...: a new run
+            render(long(rng.below(50)), frames, key);
+        } else if (r < 87) {
+            render(lastFF, 1 + int(rng.below(3)), key);  // frames per batch change
+        } else if (r < 92) {
+            render(long(rng.below(1000)), frames, key);  // frames out of pattern
+        } else {
+            flushChain();  // a reader: the run's last combines
+        }
+    }
+
+    // ---- device ------------------------------------------------------------------------------------
+    const Item &cur() const { return stream[head]; }
+    bool deviceIdle() const { return head >= stream.size(); }
+
+    void startItem() {
+        Item &it = stream[head];
+        it.started = true;
+        if (it.kind == kReset) {
+            std::fill(markers.begin(), markers.end(), 0ull);
+            std::fill(counter.begin(), counter.end(), 0u);
+            cword[0] = cword[1] = 0;
+            std::memset(copy, 0, sizeof copy);
+            std::memset(claim, 0, sizeof claim);
+            ++head;
+            return;
+        }
+        if (it.kind == kFlush) {
+            const unsigned c0 = cword[(it.epoch + 1u) & 1u];
+            for (long b = long(c0); b <= long(it.lastSeq); ++b) combineBatch(it, unsigned(b), it.epoch);
+            ++head;
+            return;
+        }
+        active = true;
+        planSet = false;
+        waves.assign(blocks * wavesPerBlock, Wave{});
+        for (size_t w = 0; w < waves.size(); ++w) waves[w].block = int(w / wavesPerBlock);
+        views.assign(blocks, View{});
+        blockBegun.assign(blocks, false);
+        // block 0's first wave's bookkeeping (chain_begin, before its waves trace): the launch's
+        // combine range for the next launch and the counters of the slots it combines
+        beginPlanFor(it, plan, planC0);
+        planSet = true;
+        cword[it.epoch & 1u] = begin_next_c0(planC0, plan.c1);
+        for (long b = long(planC0); b <= long(plan.c1); ++b) counter[unsigned(b) & (slots - 1u)] = 0;
+        combNext = long(planC0);
+        for (unsigned g = 0; g < it.group && plan.u == it.own; ++g) markers[(it.own + g) & (slots - 1u)] = marker_of(it.own + g, it.epoch);
+    }
+    static unsigned long long marker_of(unsigned t, unsigned e) { return hippt::chain::marker(t, e); }
+
+    void beginPlanFor(const Item &it, BeginPlan &p, unsigned &c0) {
+        c0 = cword[(it.epoch + 1u) & 1u];
+        const unsigned t0 = begin_t0(c0, it.own);
+        unsigned nfin = 0;
+        for (unsigned k = 0; k < 64; ++k) {
+            bool fin = false;
+            if (begin_lane_in_window(k, t0, c0, it.slots)) {
+                const unsigned t = t0 + k;
+                fin = marker_finished(markers[t & (it.slots - 1u)], t, &R == &kOwnMarkers ? it.epoch + 1u : it.epoch);
+            }
+            if (!fin) break;
+            ++nfin;
+        }
+        p = begin_plan(c0, it.own, nfin, it.slots, it.cap);
+    }
+
+    void beginBlock(int b) {
+        const Item &it = cur();
+        blockBegun[size_t(b)] = true;
+        BeginPlan p;
+        unsigned c0;
+        beginPlanFor(it, p, c0);
+        if (c0 != planC0 || p.c1 != plan.c1 || p.u != plan.u || p.tLim != plan.tLim)
+            V.add("plan", "a block's plan differs from block 0's " + where());
+        View &v = views[size_t(b)];
+        v.last = it.posted;
+        v.flags = R.startFlags(it.step);
+        v.stamp = 0;
+        v.busy = 0;
+        for (unsigned w = 0; w < wavesPerBlock; ++w) {
+            Wave &W = waves[size_t(b) * wavesPerBlock + w];
+            W.tLim = p.tLim;
+            W.posted = it.posted + 1u;
+            W.step = it.step;
+            W.t = p.u == it.own ? it.own : p.u - 1u;
+            W.stat = p.u == it.own ? it.own : ~0u;
+            // the own batch (group) untaken: its queue; else nothing to fetch, the first refill
+            // moves the wave into batch u (chain_begin: Q.left = 0)
+            W.pc = p.u == it.own ? Wave::kTrace : Wave::kNext;
+        }
+    }
+
+    void traceUnit(Wave &W, unsigned tItem, unsigned q) {
+        const Item &it = cur();
+        const long frame = it.ownFrame + long(frame_add(tItem, it.own, W.step));
+        auto key_ = std::make_pair(it.run, tItem);
+        auto tr = truth.find(key_);
+        if (tr == truth.end()) {
+            V.add("phantom", "a wave traced a batch the host never made " + where());
+            return;
+        }
+        if (frame != tr->second)
+            V.add("frame", "batch " + std::to_string(tItem) + " traced with frame " + std::to_string(frame) + " (host: " +
+                               std::to_string(tr->second) + ") " + where());
+        auto &cnt = traced[key_];
+        if (q >= cnt.size()) {
+            V.add("unit", "unit out of range " + where());
+            return;
+        }
+        ++cnt[q];
+        if (combined.count(key_)) V.add("late-trace", "a combined batch traced again " + where());
+        Slot &s = scratch[tItem & (slots - 1u)][q];
+        s.valid = true;
+        s.run = it.run;
+        s.batch = tItem;
+        s.frame = frame;
+    }
+
+    void combineBatch(const Item &it, unsigned b, unsigned epoch) {
+        auto key_ = std::make_pair(it.run, b);
+        auto tr = truth.find(key_);
+        if (tr == truth.end()) {
+            V.add("phantom-combine", "combine of a batch the host never made " + where());
+            return;
+        }
+        if (combined[key_]++) V.add("double-combine", "batch " + std::to_string(b) + " combined twice " + where());
+        if (nextCombine[it.run] != long(b))
+            V.add("order", "batch " + std::to_string(b) + " combined out of order " + where());
+        nextCombine[it.run] = long(b) + 1;
+        const long f0 = it.runFirst + long(b) * long(it.step > 0 ? it.step : 0);
+        if (f0 != tr->second) V.add("combine-frame", "combine of batch " + std::to_string(b) + " with wrong frames " + where());
+        auto &cnt = traced[key_];
+        for (unsigned q = 0; q < cnt.size(); ++q) {
+            if (cnt[q] != 1) V.add("untraced", "batch " + std::to_string(b) + " combined before it was traced " + where());
+            const Slot &s = scratch[b & (slots - 1u)][q];
+            if (!s.valid || s.run != it.run || s.batch != b || s.frame != tr->second)
+                V.add("slot", "ring slot of batch " + std::to_string(b) + " overwritten before its combine " + where());
+        }
+        (void)epoch;
+    }
+
+    // one micro-step of wave W (the kernel's refill / chain_next / chain_ask)
+    void waveStep(Wave &W) {
+        const Item &it = cur();
+        View &v = views[size_t(W.block)];
+        const unsigned xcd = unsigned(W.block) % 8u;
+        switch (W.pc) {
+        case Wave::kTrace: {
+            // the wave's pool first (a claim of `chunk` units, handed out over several refills: the
+            // rest of the launch and the host may move on meanwhile), then a claim on the counter
+            if (W.pool.empty()) {
+                const bool grp = W.t == W.stat;
+                const unsigned nb = grp ? it.group : 1u;
+                unsigned &ctr = counter[W.t & (slots - 1u)];
+                const unsigned m0 = ctr;
+                ctr += chunk;
+                for (unsigned m = m0; m < m0 + chunk && m < nb * units; ++m) {
+                    unsigned raw, tItem;
+                    group_item(m << 6, W.t, nb, raw, tItem);
+                    W.pool.push_back({tItem, raw >> 6});
+                }
+                if (W.pool.empty()) {
+                    W.pc = Wave::kNext;  // drained
+                    break;
+                }
+            }
+            W.pending.push_back(W.pool.front());
+            W.pool.erase(W.pool.begin());
+            if (W.pending.size() >= W.want) endRefill(W, Wave::kPaths);
+            break;
+        }
+        case Wave::kNext: {
+            W.nt = next_batch(W.t, W.stat, it.group);
+            if (W.nt > W.tLim) {
+                endRefill(W, Wave::kDone);
+            } else if (W.nt < W.posted) {
+                take(W, W.step);
+            } else {
+                W.askT0 = unsigned(now);
+                W.pc = Wave::kAskTopLast;
+            }
+            break;
+        }
+        case Wave::kAskTopLast:
+            W.last = v.last;
+            W.pc = Wave::kAskTopFlags;
+            break;
+        case Wave::kAskTopFlags: {
+            W.flags = v.flags;
+            const unsigned st = v.stamp;
+            if (W.nt <= W.last || (W.flags & kClosed) || (st != 0u && unsigned(now) - st < kViewRefresh)) {
+                W.pc = Wave::kAnswer;
+            } else if (v.busy == 0u) {
+                v.busy = 1u;
+                W.pc = Wave::kClaimed;
+            } else {
+                W.pc = Wave::kWait;
+            }
+            break;
+        }
+        case Wave::kWait:
+            if (v.busy == 0u || unsigned(now) - W.askT0 >= kWaitBusy) W.pc = Wave::kWaitLast;
+            break;
+        case Wave::kWaitLast:
+            W.last = v.last;
+            W.pc = Wave::kWaitFlags;
+            break;
+        case Wave::kWaitFlags:
+            W.flags = v.flags;
+            W.pc = Wave::kAnswer;
+            break;
+        case Wave::kClaimed:
+            if (R.rereadAfterClaim) {
+                W.last = v.last;
+                W.flags = v.flags;
+            }
+            W.pc = Wave::kCopyRead;
+            break;
+        case Wave::kCopyRead: {
+            const unsigned ep = it.epoch & 63u;
+            W.c = copy[xcd];
+            const unsigned age = (unsigned(now >> 4) - unsigned(W.c >> 40)) & 0xffffffu;
+            const bool ours = (unsigned(W.c >> 34) & 63u) == ep;
+            if (copy_last(W.c) < W.nt && !copy_closed(W.c) && (!ours || age >= kBoxRefresh / 16u)) {
+                const unsigned long long prev = claim[xcd];
+                const bool activeClaim = (unsigned(prev) & 63u) == ep && now - (prev & ~63ull) < kBoxRefresh;
+                if (!activeClaim) {
+                    claim[xcd] = (now & ~63ull) | ep;
+                    W.pc = Wave::kRefresh;
+                } else {
+                    W.until = now + kClaimWait;
+                    W.pc = Wave::kClaimSleep;
+                }
+            } else {
+                W.pc = Wave::kMerge;
+            }
+            break;
+        }
+        case Wave::kRefresh:  // the host word, read now (PCIe), into the per-XCD copy
+            W.c = copy_pack(now, box, it.run, it.epoch & 63u);
+            copy[xcd] = W.c;
+            W.pc = Wave::kMerge;
+            break;
+        case Wave::kClaimSleep:
+            if (now >= W.until) {
+                W.c = copy[xcd];
+                W.pc = Wave::kMerge;
+            }
+            break;
+        case Wave::kMerge:
+            if (copy_closed(W.c)) ++stats[0];
+            R.merge(W.last, W.flags, W.c);
+            W.pc = Wave::kWriteFlags;
+            break;
+        case Wave::kWriteFlags:
+            v.flags = W.flags;
+            W.pc = Wave::kWriteLast;
+            break;
+        case Wave::kWriteLast:
+            v.last = W.last;
+            W.pc = Wave::kRelease;
+            break;
+        case Wave::kRelease:
+            v.stamp = unsigned(now) ? unsigned(now) : 1u;
+            v.busy = 0u;
+            W.pc = Wave::kAnswer;
+            break;
+        case Wave::kAnswer: {
+            int step = W.step;
+            if (W.flags & kClosed) ++stats[1];
+            if (R.takes(W.nt, W.last, W.flags, it.frames, step)) {
+                if (W.flags & kClosed) {
+                    ++stats[2];
+                    W.closedTake = true;
+                    if (std::getenv("CHAIN_MODEL_DEBUG"))
+                        std::fprintf(stderr, "closed take: nt %u last %u flags %u step %d -> %d own %u ctr %u/%u\n", W.nt,
+                                     W.last, W.flags, W.step, step, it.own, counter[W.nt & (slots - 1u)], units);
+                }
+                W.posted = W.last + 1u;
+                take(W, step);
+            } else {
+                // chain_next false: the wave goes on with its lanes' paths and asks again at a later
+                // refill, or its lanes finish and it exits
+                endRefill(W, rng.chance(retryRate) ? Wave::kRetry : Wave::kDone);
+                W.until = now + 200 + rng.below(3000);
+            }
+            break;
+        }
+        case Wave::kRetry:
+            if (now >= W.until) {
+                W.want = 1 + rng.below(6);
+                W.pc = Wave::kNext;
+            }
+            break;
+        case Wave::kPaths:
+            if (now >= W.until) {
+                W.want = 1 + rng.below(6);
+                W.pc = Wave::kTrace;
+            }
+            break;
+        case Wave::kDone:
+            break;
+        }
+    }
+
+    // The end of a refill (hippt_kernels.hip, the CHAIN regen loop): the camera rays of every item the
+    // refill took — of the batch the wave was in and of the batches chain_next moved it into — are
+    // made with the wave's step as it is now (camera_sample after the loop).
+    void endRefill(Wave &W, Wave::Pc next) {
+        for (auto &u : W.pending) traceUnit(W, u.first, u.second);
+        W.pending.clear();
+        // the units' paths: the wave asks for items again once its lanes need them (a wave with
+        // long paths lags the others by batches)
+        W.until = now + (rng.below(8) == 0 ? rng.below(40000) : rng.below(400));
+        W.pc = next;
+    }
+
+    void take(Wave &W, int step) {
+        const Item &it = cur();
+        if (W.step >= 0 && step != W.step) {
+            V.add("step-change", "a wave's known step changed " + where());
+            if (std::getenv("CHAIN_MODEL_DEBUG"))
+                std::fprintf(stderr, "step change %d -> %d: t %u nt %u own %u pending %zu\n", W.step, step, W.t, W.nt,
+                             it.own, W.pending.size());
+        }
+        W.step = step;
+        W.t = W.nt;
+        markers[W.t & (slots - 1u)] = marker_of(W.t, it.epoch);
+        W.pc = Wave::kTrace;
+    }
+
+    bool launchDone() const {
+        for (bool b : blockBegun)
+            if (!b) return false;
+        for (const Wave &W : waves)
+            if (W.pc != Wave::kDone) return false;
+        return combNext > long(plan.c1);
+    }
+
+    // one device micro-step; false when there is nothing to do
+    bool deviceStep() {
+        if (!active) {
+            if (deviceIdle()) return false;
+            startItem();
+            return true;
+        }
+        const Item &it = cur();
+        // pick a block to begin, the combiner, or a wave
+        std::vector<int> choices;
+        for (unsigned b = 0; b < blocks; ++b)
+            if (!blockBegun[b]) choices.push_back(-1 - int(b));
+        if (combNext <= long(plan.c1)) choices.push_back(-1000);
+        for (size_t w = 0; w < waves.size(); ++w)
+            if (blockBegun[size_t(waves[w].block)] && waves[w].pc != Wave::kDone) choices.push_back(int(w));
+        if (choices.empty()) {
+            if (!launchDone()) V.add("stuck", "launch cannot finish " + where());
+            active = false;
+            ++head;
+            return true;
+        }
+        const int c = choices[rng.below(unsigned(choices.size()))];
+        if (c == -1000) {
+            combineBatch(it, unsigned(combNext), it.epoch);
+            ++combNext;
+        } else if (c < 0) {
+            beginBlock(-1 - c);
+        } else {
+            waveStep(waves[size_t(c)]);
+        }
+        return true;
+    }
+
+    void run(int hostOps) {
+        int done = 0;
+        while (done < hostOps) {
+            now += rng.below(4) == 0 ? rng.below(3000) : rng.below(120);
+            if (rng.chance(hostRate) || deviceIdle()) {
+                hostOp();
+                ++done;
+            } else {
+                deviceStep();
+            }
+        }
+        flushChain();
+        for (long guard = 0; deviceStep(); ++guard) {
+            now += rng.below(200);
+            if (guard > 50000000) {
+                V.add("stuck", "device never drains " + where());
+                return;
+            }
+        }
+        // every batch of every run traced once and combined once
+        for (auto &kv : traced) {
+            for (int n : kv.second)
+                if (n != 1) V.add("trace-count", "a unit traced " + std::to_string(n) + " times " + where());
+            if (combined[kv.first] != 1) V.add("combine-count", "a batch not combined exactly once " + where());
+        }
+    }
+};
+
+static int directed() {
+    // The GPUTEST_r05 interleaving at the level of one block's view (VERDICT r5 "What's weak" 1):
+    // a launch of batch 0 (chainStep -1, view last 0), the view refreshed while the run is open
+    // (batches up to 3 posted, consecutive frames), then refreshed once the host is on a later run
+    // (closed), then a wave that drained batch 1 asks for batch 2 <= last.
+    const unsigned run = 7, frames = 1;
+    int bad = 0;
+    for (const Rules *R : {&kLegacy, &kFixed}) {
+        unsigned last = 0, flags = R->startFlags(-1);
+        R->merge(last, flags, copy_pack(5000, box_word(run, true, 3), run, 0));
+        R->merge(last, flags, copy_pack(9000, box_word(run + 1, false, 0), run, 0));
+        int step = -1;
+        const bool took = R->takes(2, last, flags, int(frames), step);
+        const bool right = took && step == int(frames);
+        std::printf("%s: last %u flags %u took %d step %d -> %s\n", R->name, last, flags, int(took), step,
+                    right ? "frames of batch 2 right" : "batch 2 traced with batch 0's frames");
+        if (R == &kFixed && !right) bad = 1;
+        if (R == &kLegacy && right) bad = 1;  // the model must show the recorded failure
+    }
+    return bad;
+}
+
+int main(int argc, char **argv) {
+    if (argc >= 2 && std::strcmp(argv[1], "directed") == 0) return directed();
+    if (argc < 3) {
+        std::fprintf(stderr, "usage: chain_model fixed|legacy|small-ring|own-markers SEEDS [FIRST_SEED] | directed\n");
+        return 2;
+    }
+    const Rules *rules[] = {&kFixed, &kLegacy, &kSmallRing, &kOwnMarkers};
+    const Rules *pick = nullptr;
+    for (const Rules *r : rules)
+        if (std::strcmp(argv[1], r->name) == 0) pick = r;
+    if (!pick) {
+        std::fprintf(stderr, "unknown rules %s\n", argv[1]);
+        return 2;
+    }
+    const Rules &R = *pick;
+    const long seeds = std::atol(argv[2]);
+    const long first = argc > 3 ? std::atol(argv[3]) : 1;
+    Violations V;
+    long scenarios = 0, launches = 0, batches = 0, st[4] = {0, 0, 0, 0};
+    for (long s = first; s < first + seeds; ++s) {
+        const long before = V.total();
+        Model m(R, uint64_t(s), V);
+        m.run(12 + int(s % 40));
+        if (V.total() != before && std::getenv("CHAIN_MODEL_SEEDS")) std::fprintf(stderr, "seed %ld\n", s);
+        ++scenarios;
+        for (auto &it : m.stream) launches += it.kind == kLaunch;
+        batches += long(m.truth.size());
+        for (int k = 0; k < 4; ++k) st[k] += m.stats[k];
+    }
+    std::printf("rules %s violations %ld scenarios %ld launches %ld batches %ld", R.name, V.total(), scenarios,
+                launches, batches);
+    std::printf(" closed_merges %ld closed_answers %ld closed_takes %ld", st[0], st[1], st[2]);
+    for (auto &kv : V.n) std::printf(" %s=%ld", kv.first.c_str(), kv.second);
+    std::printf("\n");
+    if (!V.first.empty()) std::printf("first: %s\n", V.first.c_str());
+    return 0;
+}

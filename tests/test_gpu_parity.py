@@ -9,6 +9,7 @@ import os
 import numpy as np
 import pytest
 
+import chain_audit
 import hippt
 import pyoracle as po
 from hippt import scenes
@@ -18,6 +19,12 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture()
 def pt():
+    """The library's defaults, except that the item order is computed on the render path
+    (HIPPT_OPT_ITEM_ORDER 1) rather than by the detached cost job of the automatic mode, so that
+    host timing does not choose the code path a test runs (a green run then proves only
+    one interleaving); the automatic mode has tests of its own.  Every chained run of every test is
+    audited (HIPPT_OPT_CHAIN_AUDIT, tests/chain_audit.py): each batch traced once with its own frames,
+    combined once, in order."""
     t = hippt.PathTracer()
     t.setDevices([])
     t.setRowRange(0, 0)
@@ -30,12 +37,18 @@ def pt():
                  (hippt.OPT_STACK_CAP, 0), (hippt.OPT_BVH_QUANT, -1), (hippt.OPT_LDS_TOP_NODES, -1),
                  (hippt.OPT_RNG_TABLE, 0), (hippt.OPT_BVH_COLLAPSE, -1), (hippt.OPT_BVH_NODE_COST, 200),
                  (hippt.OPT_BVH_LEAF4, 4), (hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_ARGB),
-                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1), (hippt.OPT_ITEM_ORDER, -1),
-                 (hippt.OPT_WAVEFRONT_SORT, -1), (hippt.OPT_CHAIN, -1)):
+                 (hippt.OPT_CAMERA_POOL, -1), (hippt.OPT_FUSE_COMBINE, -1), (hippt.OPT_ITEM_ORDER, 1),
+                 (hippt.OPT_WAVEFRONT_SORT, -1), (hippt.OPT_CHAIN, -1), (hippt.OPT_CHAIN_AUDIT, 1)):
         t.setOption(k, v)
     t.resetStats()
+    hippt.chain_audit()  # (drops records of earlier tests)
     yield t
+    runs = hippt.chain_audit()
+    t.setOption(hippt.OPT_CHAIN_AUDIT, 0)
     hippt.load_library().cudaPathTracerShutdown()
+    t.audited = runs
+    problems = chain_audit.check(runs)
+    assert not problems, f"{len(problems)} chain audit problems in {len(runs)} runs: {problems[:6]}"
 
 
 def _assert_same(gpu_px, gpu_acc, ora_px, ora_acc):
@@ -640,8 +653,9 @@ def test_mesh_batches_and_frame_splits_are_bit_identical(pt):
     _assert_same(one[0], one[1], split[0], split[1])
 
 
+@pytest.mark.parametrize("order", [0, 1])
 @pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene", "cornell_mixed"])
-def test_chained_batches_match_oracle(pt, name):
+def test_chained_batches_match_oracle(pt, name, order):
     """HIPPT_OPT_CHAIN (Ctx::chain, hippt_trace.h chained batches): a launch whose batch is drained
     goes on with the asynchronous batches posted behind it, the next launch combines them beside its
     own paths, and the image's readers flush the rest.  At caps 1, 2 and 8, off and automatic, the
@@ -656,6 +670,7 @@ def test_chained_batches_match_oracle(pt, name):
     ora6 = po.MeshScene(sc, w, h).frames(0, 6, 8)
     ora2 = po.MeshScene(sc, w, h).frames(0, 2, 8)
     pt.uploadMesh(sc)
+    pt.setOption(hippt.OPT_ITEM_ORDER, order)
     lib = hippt.load_library()
     for chain in (1, 2, 8, 0, -1):
         pt.setOption(hippt.OPT_CHAIN, chain)
@@ -780,8 +795,122 @@ def test_chained_batches_with_skipped_launches(pt):
         _assert_same(images[chain][0], images[chain][1], images[0][0], images[0][1])
 
 
+def _moved_camera(sc, w, h, dx=40.0, dy=25.0):
+    return hippt.build_camera(lookfrom=(sc.lookfrom[0] + dx, sc.lookfrom[1] + dy, sc.lookfrom[2]), lookat=sc.lookat,
+                              vup=sc.vup, vfov=sc.vfov, aspect=w / h, aperture=sc.aperture, focus=sc.focus)
+
+
+def _audited_runs(min_batches=2):
+    runs = hippt.chain_audit()
+    problems = chain_audit.check(runs)
+    assert not problems, problems[:6]
+    return [r for r in runs if r[0]["batches"] >= min_batches]
+
+
+@pytest.mark.parametrize("order", [0, 1])
+@pytest.mark.parametrize("name", ["blob70k", "cornell34"])
+def test_run_closes_while_a_launch_runs(pt, name, order):
+    """a run that closes while its launch still runs.  Four long progressive
+    batches (256x144 x 512 frames: the first launch runs for milliseconds and takes the posted batches
+    behind it, the later ones are held), then a camera change (a new run: the host's mailbox moves on
+    while the old run's waves are still inside their batches, some holding claimed items), a burst of
+    small batches of the new camera, and the readback's flush.  The image and accumulation equal one
+    launch per batch (HIPPT_OPT_CHAIN 0) bit for bit, two rows equal the oracle's continuation across
+    the camera change, and the audit finds every batch of both runs traced once with its own frames
+    and combined once, in order."""
+    import ctypes
+    sc = scenes.get_scene(name)
+    w, h = 256, 144
+    lib = hippt.load_library()
+    err = ctypes.c_char_p()
+    pt.setOption(hippt.OPT_ITEM_ORDER, order)
+    cam = _moved_camera(sc, w, h)
+    images = {}
+    for chain in (-1, 0):
+        pt.setOption(hippt.OPT_CHAIN, chain)
+        pt.uploadMesh(sc)
+        assert pt.initialize(w, h), pt.lastError()
+        pt.resetStats()
+        for _ in range(4):
+            assert pt.renderFramesAsync(512, 8), pt.lastError()
+        assert lib.hipptSetCamera(ctypes.byref(cam), ctypes.byref(err)), err.value
+        for _ in range(6):
+            assert pt.renderFramesAsync(4, 8), pt.lastError()
+        images[chain] = pt.readback()
+        assert pt.stats()["pixelSamples"] == w * h * (4 * 512 + 6 * 4)
+        if chain == -1:
+            runs = _audited_runs()
+            assert any(r[0]["batches"] == 4 and r[0]["totalItems"] == w * h * 512 for r in runs), \
+                [r[0] for r in runs]
+    _assert_same(images[-1][0], images[-1][1], images[0][0], images[0][1])
+    ms = po.MeshScene(sc, w, h)
+    ys = (57, 58)
+    a = ms.frames(0, 4 * 512, 8, y0=ys[0], y1=ys[1] + 1)
+    moved = po.MeshScene(sc, w, h, cam=po.PoCamera.from_buffer_copy(bytes(cam)))
+    b = moved.frames(4 * 512, 6 * 4, 8, y0=ys[0], y1=ys[1] + 1, accum=a[1])
+    _assert_same(images[-1][0][ys[0]:ys[1] + 1], images[-1][1][ys[0]:ys[1] + 1], b[0], b[1])
+
+
+@pytest.mark.parametrize("event", ["upload", "pixel_format", "blocks_per_cu", "readback"])
+def test_held_group_closed_by_event(pt, event):
+    """a run whose batches are held (arrived while the run's last launch had not started)
+    and is then closed by a scene upload (its buffers freed and replaced: the held group launches
+    first, ensure_scene), a pixel-format change, a grid change or a readback.  The image equals one
+    launch per batch and the audit is clean."""
+    sc, other = scenes.blob70k(), scenes.cornell34()
+    w, h = 192, 108
+    images = {}
+    for chain in (-1, 0):
+        pt.setOption(hippt.OPT_CHAIN, chain)
+        pt.setOption(hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_ARGB)
+        pt.setOption(hippt.OPT_BLOCKS_PER_CU, 0)
+        pt.uploadMesh(sc)
+        assert pt.initialize(w, h), pt.lastError()
+        for _ in range(5):  # the first launch runs while the next batches arrive: held
+            assert pt.renderFramesAsync(256, 8), pt.lastError()
+        if event == "upload":
+            pt.uploadMesh(other)
+        elif event == "pixel_format":
+            pt.setOption(hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_RGBA8)
+        elif event == "blocks_per_cu":
+            pt.setOption(hippt.OPT_BLOCKS_PER_CU, 2)
+        else:
+            images[(chain, "mid")] = pt.readback()
+        for _ in range(3):
+            assert pt.renderFramesAsync(256, 8), pt.lastError()
+        images[chain] = pt.readback()
+        if chain == -1:
+            assert _audited_runs(), "no chained run"
+    pt.setOption(hippt.OPT_PIXEL_FORMAT, hippt.PIXEL_ARGB)
+    pt.setOption(hippt.OPT_BLOCKS_PER_CU, 0)
+    _assert_same(images[-1][0], images[-1][1], images[0][0], images[0][1])
+    if event == "readback":
+        _assert_same(images[(-1, "mid")][0], images[(-1, "mid")][1], images[(0, "mid")][0], images[(0, "mid")][1])
+
+
+def test_chain_ring_within_scratch_budget(pt):
+    """the chain ring (slots x 2^shift samples x 12 B) stays within HIPPT_OPT_SCRATCH_MB: a
+    budget under two slots runs the batches unchained (HIPPT_INFO_CHAIN_CAP 0), a budget of two slots
+    chains with cap 1, a larger one with the automatic cap; the images are the oracle's."""
+    sc = scenes.cornell34()
+    w, h = 160, 90  # 8 frames: 115200 items, 2^17-sample slots of 1.5 MiB
+    ora = po.MeshScene(sc, w, h).frames(0, 24, 8)
+    pt.uploadMesh(sc)
+    lib = hippt.load_library()
+    for mb, cap in ((1, 0), (4, 1), (64, 8)):
+        pt.setOption(hippt.OPT_SCRATCH_MB, mb)
+        assert pt.initialize(w, h), pt.lastError()
+        for _ in range(3):
+            assert pt.renderFramesAsync(8, 8), pt.lastError()
+        got = pt.readback()
+        _assert_same(got[0], got[1], ora[0], ora[1])
+        assert lib.hipptGetOption(hippt.INFO_CHAIN_CAP) == cap, mb
+    pt.setOption(hippt.OPT_SCRATCH_MB, 32768)
+
+
+@pytest.mark.parametrize("order", [0, 1])
 @pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene"])
-def test_deferred_combine_across_async_calls(pt, name):
+def test_deferred_combine_across_async_calls(pt, name, order):
     """Back-to-back hipptRenderFramesAsync calls: each megakernel batch's combine (running average
     + tonemap) runs inside the next batch's launch (Ctx::deferred), from the other scratch buffer;
     anything that reads or resets the image runs the pending one first.  Every sequence below
@@ -790,6 +919,7 @@ def test_deferred_combine_across_async_calls(pt, name):
     w, h = 45, 26
     ora6 = po.MeshScene(sc, w, h).frames(0, 6, 8)
     pt.uploadMesh(sc)
+    pt.setOption(hippt.OPT_ITEM_ORDER, order)
     # fused off: every batch's combine its own launch
     pt.setOption(hippt.OPT_FUSE_COMBINE, 0)
     assert pt.initialize(w, h)
