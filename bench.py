@@ -32,9 +32,10 @@ Also reported on rank 0:
                 algorithmic_bytes = the SURVEY.md 8(d) node/primitive/shading bytes (served by
                 LDS/L2/MALL, not HBM).
   cpu_baseline  the reference CPU path tracer (RayTracer.h + Qt-free RenderWorker, built as
-                oracle/_ref/ref_harness) timed on this box's host cores over a bounded row
-                sample of the same workload: the median of 3 runs, with the host's CPU facts
-                (nproc, the affinity mask's size, lscpu's model name, OMP_NUM_THREADS).  If the
+                oracle/_ref/ref_harness) timed on this box's host cores over a bounded sample
+                of whole rows of the same workload: the median of 5 runs at the box's CPU share,
+                a 1-thread rate and the projection to the affinity mask, with the host's CPU
+                facts (nproc, the affinity mask's size, lscpu's model name, OMP_NUM_THREADS).  If the
                 harness is missing the object says so (value null, an error string) instead of
                 timing a different program; --cpu-baseline port times the FP32 oracle port.
 """
@@ -111,8 +112,8 @@ def parse():
     p.add_argument("--bvh-width", type=int, default=None, choices=[0, 2, 4],
                    help="megakernel BVH width (HIPPT_OPT_BVH_WIDTH; default automatic)")
     p.add_argument("--cpu-baseline", default="auto", choices=["auto", "reference", "port", "off"])
-    p.add_argument("--cpu-seconds", type=float, default=8.0, help="target duration of one CPU sample run")
-    p.add_argument("--cpu-runs", type=int, default=3, help="CPU sample runs (the median is reported)")
+    p.add_argument("--cpu-seconds", type=float, default=6.0, help="target duration of one CPU sample run")
+    p.add_argument("--cpu-runs", type=int, default=5, help="CPU sample runs (the median is reported)")
     p.add_argument("--cpu-threads", type=int, default=None)
     p.add_argument("--option", action="append", default=[], metavar="NAME=V",
                    help="any library option by its hippt.h name without HIPPT_OPT_ (e.g. BVH_QUANT=3); "
@@ -182,28 +183,49 @@ def cpu_baseline(args, scene) -> dict | None:
             path = os.path.join(tmp, "scene.bin")
             sc_mod.write_scene_file(scene, path)
 
-            def run(stride):
+            def sample(n_threads, seconds, n_runs):
+                # probe on every 64th line, then pick the line stride that takes ~seconds
+                probe = run_t(64, n_threads)
+                per_line = probe["seconds"] / max(1, probe["rows"])
+                lines = max(1, min(args.height, int(seconds / max(per_line, 1e-6))))
+                stride = max(1, -(-args.height // lines))
+                return stride, sorted((run_t(stride, n_threads) for _ in range(n_runs)),
+                                      key=lambda r: r["msamples_per_s"])
+
+            def run_t(stride, n_threads):
                 out = subprocess.run([pyoracle.REF_HARNESS, "bench", path, str(args.width), str(args.height),
-                                      str(stride), str(args.spp), str(args.depth), str(threads)],
+                                      str(stride), str(args.spp), str(args.depth), str(n_threads)],
                                      capture_output=True, text=True, check=True, timeout=900).stdout
                 return json.loads(out.strip().splitlines()[-1])
 
-            # probe on every 64th line, then pick the line stride that takes ~cpu_seconds
-            probe = run(64)
-            per_line = probe["seconds"] / max(1, probe["rows"])
-            lines = max(1, min(args.height, int(args.cpu_seconds / max(per_line, 1e-6))))
-            stride = max(1, -(-args.height // lines))
-            rs = sorted((run(stride) for _ in range(runs)), key=lambda r: r["msamples_per_s"])
+            stride, rs = sample(threads, args.cpu_seconds, runs)
+            # per-thread rate (1 thread, fewer lines) and the parallel efficiency of the share, for the
+            # projection to the whole affinity mask (the reference uses hardware_concurrency() threads,
+            # RayTracerFboItem.cpp:75; the GPU box's CPU share is OMP_NUM_THREADS = 16 per GPU and a run
+            # must not use more, so the mask-wide figure is projected, not timed)
+            one = None
+            if threads > 1 and facts["affinity"] > threads and args.cpu_runs > 1:
+                _, r1 = sample(1, args.cpu_seconds / 2, 3)
+                one = r1[len(r1) // 2]
         r = rs[len(rs) // 2]
-        return {"value": round(r["msamples_per_s"], 4), "unit": "Msamples/s", "cores": threads,
-                "kind": "reference",
-                "sample": f"every {stride}th line ({r['rows']} lines) of {args.width}x{args.height}, {args.spp} spp, "
-                          f"depth {args.depth}, "
-                          f"{scene.name}; RayTracer.h ray_color + RenderWorker tile pool (tile {r['tile']}), "
-                          f"{r['segments']} segments in {r['seconds']:.2f} s; median of {runs} runs",
-                "runs": [round(x["msamples_per_s"], 4) for x in rs],
-                "threads_rule": rule, "host": facts,
-                "mpixel_samples_per_s": round(r["mpixel_samples_per_s"], 4)}
+        out = {"value": round(r["msamples_per_s"], 4), "unit": "Msamples/s", "cores": threads,
+               "kind": "reference",
+               "sample": f"every {stride}th line ({r['rows']} whole lines) of {args.width}x{args.height}, {args.spp} spp, "
+                         f"depth {args.depth}, "
+                         f"{scene.name}; RayTracer.h ray_color + RenderWorker tile pool (tile {r['tile']}), "
+                         f"{r['segments']} segments in {r['seconds']:.2f} s; median of {runs} runs",
+               "runs": [round(x["msamples_per_s"], 4) for x in rs],
+               "threads_rule": rule, "host": facts,
+               "mpixel_samples_per_s": round(r["mpixel_samples_per_s"], 4)}
+        if one:
+            eff = r["msamples_per_s"] / (threads * one["msamples_per_s"])
+            out["per_thread"] = {"value": round(one["msamples_per_s"], 4), "threads": 1,
+                                 "parallel_efficiency_at_cores": round(eff, 3)}
+            out["full_affinity_projected"] = {
+                "value": round(one["msamples_per_s"] * facts["affinity"] * eff, 2), "threads": facts["affinity"],
+                "rule": "1-thread rate x affinity-mask threads x the measured parallel efficiency at `cores` "
+                        "threads (projected: the box's CPU share is `cores`; not timed at the mask's size)"}
+        return out
     ms = pyoracle.MeshScene(scene, args.width, args.height, accel=1)
     t0 = time.perf_counter()
     _, _, segs, ps = ms.frames(0, args.spp, args.depth, y0=0, y1=2, nthreads=threads)

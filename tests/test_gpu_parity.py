@@ -893,15 +893,15 @@ def test_chain_ring_within_scratch_budget(pt):
     budget under two slots runs the batches unchained (HIPPT_INFO_CHAIN_CAP 0), a budget of two slots
     chains with cap 1, a larger one with the automatic cap; the images are the oracle's."""
     sc = scenes.cornell34()
-    w, h = 160, 90  # 8 frames: 115200 items, 2^17-sample slots of 1.5 MiB
-    ora = po.MeshScene(sc, w, h).frames(0, 24, 8)
+    w, h = 640, 360  # one frame per batch: 230400 items, 2^18-sample slots of 3 MiB
+    ora = po.MeshScene(sc, w, h).frames(0, 3, 8)
     pt.uploadMesh(sc)
     lib = hippt.load_library()
-    for mb, cap in ((1, 0), (4, 1), (64, 8)):
+    for mb, cap in ((4, 0), (8, 1), (64, 8)):
         pt.setOption(hippt.OPT_SCRATCH_MB, mb)
         assert pt.initialize(w, h), pt.lastError()
         for _ in range(3):
-            assert pt.renderFramesAsync(8, 8), pt.lastError()
+            assert pt.renderFramesAsync(1, 8), pt.lastError()
         got = pt.readback()
         _assert_same(got[0], got[1], ora[0], ora[1])
         assert lib.hipptGetOption(hippt.INFO_CHAIN_CAP) == cap, mb
