@@ -75,12 +75,14 @@ constexpr bool kLegacyZeroCopy = HIPPT_LEGACY_ZERO_COPY != 0;
 // The key of a context's run-cost estimates (item order): what the estimate depends on.
 struct OrderKey {
     int version = -1, width = 0, height = 0, y0 = 0, rows = 0, stride = 0, maxDepth = 0;
+    unsigned tileShift = 6;  // the runs' shape (item_order.h RunLayout)
     CameraF cam{};
 };
 
 bool same_key(const OrderKey &a, const OrderKey &b) {
     if (a.version != b.version || a.width != b.width || a.height != b.height || a.y0 != b.y0 || a.rows != b.rows ||
-        a.stride != b.stride || a.maxDepth != b.maxDepth || a.cam.lens_radius != b.cam.lens_radius)
+        a.stride != b.stride || a.maxDepth != b.maxDepth || a.tileShift != b.tileShift ||
+        a.cam.lens_radius != b.cam.lens_radius)
         return false;
     for (int k = 0; k < 3; ++k)
         if (a.cam.origin[k] != b.cam.origin[k] || a.cam.llc[k] != b.cam.llc[k] ||
@@ -276,6 +278,7 @@ struct State {
     int cameraPool = -1;  // megakernel camera-ray pool (HIPPT_OPT_CAMERA_POOL; -1: automatic)
     int fuseCombine = -1;  // combine inside the next megakernel launch (HIPPT_OPT_FUSE_COMBINE)
     int itemOrder = -1;    // scene-hitting pixel runs first (HIPPT_OPT_ITEM_ORDER; -1: automatic)
+    int pixelTile = -1;    // the item order's runs: tile columns (HIPPT_OPT_PIXEL_TILE; 0 rows, -1 automatic)
     int chainBatches = -1; // batches a chained launch may trace (HIPPT_OPT_CHAIN; 0 off, -1 automatic)
     bool chainAudit = false;            // HIPPT_OPT_CHAIN_AUDIT
     std::vector<unsigned> auditWords;   // closed runs' audit words not yet read (hipptChainAudit)
@@ -589,11 +592,12 @@ constexpr size_t kOrderTables = 4;
 
 int cost_threads() { return int(std::max(1u, std::min(16u, std::thread::hardware_concurrency()))); }
 
-bool ensure_order(Ctx &c, const CameraF &cam, int frames, int maxDepth, bool forced, const unsigned **table,
-                  const char **err) {
+bool ensure_order(Ctx &c, const CameraF &cam, int frames, int maxDepth, bool forced, unsigned tileShift,
+                  const unsigned **table, const char **err) {
     State &s = S();
     *table = nullptr;
     OrderKey key;
+    key.tileShift = hippt::tile_shift_for(unsigned(s.width), tileShift);
     key.version = s.scene.version;
     key.width = s.width;
     key.height = s.height;
@@ -615,8 +619,9 @@ bool ensure_order(Ctx &c, const CameraF &cam, int frames, int maxDepth, bool for
             c.costJob.reset();
         } else if (forced) {
             abandon_cost_job(c);  // a stale key's job: not joined on the render path
-            hippt::run_costs(s.scene.bvh4, reinterpret_cast<const float *>(s.scene.tris.data()), cam, s.width,
-                             s.height, c.y0, c.rows, c.stride, maxDepth, cost, cost_threads());
+            hippt::run_costs(s.scene.bvh4, reinterpret_cast<const float *>(s.scene.tris.data()), cam,
+                             hippt::RunLayout{unsigned(s.width), unsigned(c.rows), key.tileShift}, s.height, c.y0,
+                             c.stride, maxDepth, cost, cost_threads());
         } else {
             if (c.costJob && !jobForKey) abandon_cost_job(c);
             if (!c.costJob) {
@@ -631,8 +636,11 @@ bool ensure_order(Ctx &c, const CameraF &cam, int frames, int maxDepth, bool for
                         // and this key's batches stay in image order
                         try {
                             hippt::run_costs(job->bvh, reinterpret_cast<const float *>(job->tris.data()),
-                                             job->key.cam, job->key.width, job->key.height, job->key.y0,
-                                             job->key.rows, job->key.stride, job->key.maxDepth, job->cost, nt);
+                                             job->key.cam,
+                                             hippt::RunLayout{unsigned(job->key.width), unsigned(job->key.rows),
+                                                              job->key.tileShift},
+                                             job->key.height, job->key.y0, job->key.stride, job->key.maxDepth,
+                                             job->cost, nt);
                         } catch (...) {
                             job->cost.clear();
                         }
@@ -664,8 +672,8 @@ bool ensure_order(Ctx &c, const CameraF &cam, int frames, int maxDepth, bool for
             return true;
         }
     std::vector<uint32_t> order;
-    hippt::build_item_table(c.runCosts, unsigned(c.rows) * unsigned(s.width), unsigned(frames), hippt::kMeshQueues,
-                            order);
+    hippt::build_item_table(c.runCosts, hippt::RunLayout{unsigned(s.width), unsigned(c.rows), c.orderKey.tileShift},
+                            unsigned(frames), hippt::kMeshQueues, order);
     unsigned *dev = nullptr;
     HIP_TRY(hipMalloc(&dev, std::max<size_t>(1, order.size()) * sizeof(unsigned)));
     // a fresh buffer: the copy need not wait for the launches queued on the context's stream
@@ -1181,7 +1189,7 @@ bool chain_same(const hippt::MeshParams &a, const hippt::MeshParams &b) {
            a.waveThreshold == b.waveThreshold && a.chunk == b.chunk && a.leafExit == b.leafExit &&
            a.nodeExit == b.nodeExit && a.wide == b.wide && a.stackCap == b.stackCap && a.spillCap == b.spillCap &&
            a.spill == b.spill && a.topBytes == b.topBytes && a.refBits == b.refBits && a.runOrder == b.runOrder &&
-           a.runCount == b.runCount && a.rngTable == b.rngTable && a.poolOffset == b.poolOffset &&
+           a.runCount == b.runCount && a.runTileShift == b.runTileShift && a.rngTable == b.rngTable && a.poolOffset == b.poolOffset &&
            a.poolWords == b.poolWords && a.comb.format == b.comb.format;
 }
 
@@ -1614,10 +1622,15 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         // +0.8% at full size; the slowest 1/8 Cornell share -2% (r5w)
                         if (s.pathMode == 0 && s.itemOrder != 0) {
                             const unsigned *table = nullptr;
-                            if (!ensure_order(c, cam, nf, maxDepth, s.itemOrder == 1, &table, err)) return false;
+                            // the runs' shape: HIPPT_OPT_PIXEL_TILE columns (automatic: rows)
+                            const unsigned tileShift = s.pixelTile == 8 ? 3u : s.pixelTile == 16 ? 4u
+                                                       : s.pixelTile == 32 ? 5u : 6u;
+                            if (!ensure_order(c, cam, nf, maxDepth, s.itemOrder == 1, tileShift, &table, err))
+                                return false;
                             if (table) {
                                 p.runOrder = table;
                                 p.runCount = unsigned(c.runCosts.size());
+                                p.runTileShift = c.orderKey.tileShift;
                             }
                         }
                         p.poolOffset = unsigned(hippt::mesh_lds_bytes(stackDepth, ldsScene ? numNodes : 0,
@@ -2394,6 +2407,10 @@ extern "C" bool hipptSetOption(int key, long long value) try {
         if (value != 0 && value != 1) return false;
         s.chainAudit = value == 1;
         return true;
+    case HIPPT_OPT_PIXEL_TILE:
+        if (value != -1 && value != 0 && value != 8 && value != 16 && value != 32) return false;
+        s.pixelTile = int(value);
+        return true;
     default: return false;
     }
 } catch (const std::exception &e) {
@@ -2445,6 +2462,7 @@ extern "C" long long hipptGetOption(int key) try {
     case HIPPT_OPT_WAVEFRONT_SORT: return s.wfSort;
     case HIPPT_OPT_CHAIN: return s.chainBatches;
     case HIPPT_OPT_CHAIN_AUDIT: return s.chainAudit ? 1 : 0;
+    case HIPPT_OPT_PIXEL_TILE: return s.pixelTile;
     case HIPPT_INFO_LDS_TOP_BYTES: return s.activeTopBytes;
     case HIPPT_INFO_BLOCKS_PER_CU: return s.activeBlocksPerCu;
     case HIPPT_INFO_CHUNK: return s.activeChunk;

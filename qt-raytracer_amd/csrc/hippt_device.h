@@ -92,10 +92,13 @@ struct MeshParams {
     // (trace::child_key_p; hippt_api.cpp packed_ref_bits)
     unsigned refBits;
     // The queues' order of the batch's items (item_order.h build_item_table): queue position
-    // fl*bandPixels + 64*j + k is item runOrder[fl*runCount + j] + k for j < runCount (runs of 64
-    // band pixels per frame); null: image order.
+    // fl*bandPixels + 64*j + k is item k of the run at runOrder[fl*runCount + j] for j < runCount
+    // (runs of 64 band pixels per frame: consecutive pixels, or a tile when flagged, item_order.h);
+    // null: image order.
     const unsigned *runOrder;
     unsigned runCount;
+    // log2 of a tile run's columns (item_order.h RunLayout; entries flagged kRunTile are tiles)
+    unsigned runTileShift;
     // random_in_unit_sphere memoized (null: the rejection loop): entry 2^32-word table, see
     // launch_rng_table
     const uint32_t *rngTable;

@@ -335,12 +335,19 @@ __device__ __forceinline__ CamArgs cam_args_late() { return late_arg_at<CamArgs>
 // The work item at queue position `it` (MeshParams::runOrder, item_order.h build_item_table):
 // the 64-item slot of (frame, run) handed out as the slot the table names, the offset within
 // the run kept; positions outside whole runs and kNone stay as they are.
+// A table entry's item k: consecutive band pixels, or (flag bit 31, item_order.h kRunTile) column
+// k mod 2^tileShift, band row k >> tileShift of a tile.
+__device__ __forceinline__ unsigned run_item(unsigned v, unsigned k, unsigned width, unsigned tileShift) {
+    return (v & 0x7fffffffu) + ((v >> 31) ? (k & ((1u << tileShift) - 1u)) + (k >> tileShift) * width : k);
+}
+
 __device__ __forceinline__ unsigned order_item(const MeshParams &P, unsigned it) {
     if (it == kNone || !P.runOrder) return it;
     unsigned fl, q;
     divmod(it, P.bandPixels, P.rcpBandPixels, fl, q);
     const unsigned run = q >> 6;
-    return run < P.runCount ? P.runOrder[fl * P.runCount + run] + (q & 63u) : it;
+    return run < P.runCount ? run_item(P.runOrder[fl * P.runCount + run], q & 63u, unsigned(P.width), P.runTileShift)
+                            : it;
 }
 
 // order_item with its arguments loaded where it runs (HIPPT_LATE_CAM)
@@ -353,7 +360,9 @@ __device__ __forceinline__ unsigned order_item_late(unsigned it) {
     unsigned fl, q;
     divmod(it, A.bandPixels, A.rcpBandPixels, fl, q);
     const unsigned run = q >> 6;
-    return run < runs ? order[fl * runs + run] + (q & 63u) : it;
+    return run < runs ? run_item(order[fl * runs + run], q & 63u, unsigned(A.width),
+                                 late_arg_at<unsigned>(unsigned(offsetof(MeshParams, runTileShift))))
+                      : it;
 }
 
 // ---- chained batches (MeshParams::chain*, CHAIN kernels) ----------------------------

@@ -134,11 +134,33 @@ double sample_cost(const Bvh4 &b, const float *tris, D3 o, D3 d, int maxDepth) {
 
 }  // namespace
 
-void run_costs(const Bvh4 &bvh, const float *tris, const CameraF &cam, int width, int height, int y0, int rows,
+unsigned tile_shift_for(unsigned width, unsigned tileShift) {
+    if (tileShift >= 6) return 6;
+    return width % (1u << tileShift) == 0 ? tileShift : 6;
+}
+
+size_t run_count(const RunLayout &L) { return size_t(L.rows) * size_t(L.width) / 64; }
+
+uint32_t run_base(const RunLayout &L, size_t r) {
+    if (L.tileShift >= 6) return uint32_t(64 * r);
+    const size_t tw = size_t(1) << L.tileShift, th = 64 / tw;
+    const size_t perStrip = L.width / tw, tileRuns = (L.rows / th) * perStrip;
+    if (r < tileRuns) return uint32_t(((r / perStrip) * th * L.width + (r % perStrip) * tw)) | kRunTile;
+    return uint32_t(tileRuns * 64 + 64 * (r - tileRuns));
+}
+
+uint32_t run_pixel(const RunLayout &L, size_t r, unsigned k) {
+    const uint32_t b = run_base(L, r);
+    if (!(b & kRunTile)) return b + k;
+    return (b & ~kRunTile) + (k & ((1u << L.tileShift) - 1u)) + (k >> L.tileShift) * L.width;
+}
+
+void run_costs(const Bvh4 &bvh, const float *tris, const CameraF &cam, const RunLayout &L, int height, int y0,
                int stride, int maxDepth, std::vector<float> &cost, int threads) {
     cost.clear();
-    if (width <= 0 || rows <= 0) return;
-    const size_t runs = size_t(rows) * size_t(width) / 64;
+    const int width = int(L.width);
+    if (width <= 0 || L.rows <= 0) return;
+    const size_t runs = run_count(L);
     const double sw = double(std::max(1, width - 1)), sh = double(std::max(1, height - 1));
     const D3 O{cam.origin[0], cam.origin[1], cam.origin[2]};
     cost.assign(runs, 0.0f);
@@ -146,7 +168,7 @@ void run_costs(const Bvh4 &bvh, const float *tris, const CameraF &cam, int width
         for (size_t r = r0; r < r1; ++r) {
             double c = 0.0;
             for (int j = 0; j < 4; ++j) {
-                const size_t p = 64 * r + size_t(21 * j);  // band pixels 0, 21, 42, 63 of the run
+                const size_t p = run_pixel(L, r, unsigned(21 * j));  // the run's items 0, 21, 42, 63
                 const double x = double(p % size_t(width)) + 0.5;
                 const double y = double(y0 + int(p / size_t(width)) * stride) + 0.5;
                 const double s = x / sw, t = y / sh;
@@ -177,13 +199,16 @@ void run_costs(const Bvh4 &bvh, const float *tris, const CameraF &cam, int width
     for (auto &t : pool) t.join();
 }
 
-void build_item_table(const std::vector<float> &cost, unsigned bandPixels, unsigned frames, unsigned queues,
+void build_item_table(const std::vector<float> &cost, const RunLayout &L, unsigned frames, unsigned queues,
                       std::vector<uint32_t> &table) {
     const size_t runs = cost.size(), slots = runs * frames;
     table.assign(slots, 0u);
     if (!slots) return;
+    const unsigned bandPixels = L.width * L.rows;
     const unsigned long long total = (unsigned long long)bandPixels * frames;
-    auto item = [&](size_t s) { return uint32_t((s / runs) * bandPixels + 64 * (s % runs)); };
+    // slot s: queue position pos(s) (which queue hands it out), items from item(s)
+    auto pos = [&](size_t s) { return (unsigned long long)(s / runs) * bandPixels + 64 * (s % runs); };
+    auto item = [&](size_t s) { return uint32_t((s / runs) * bandPixels) + run_base(L, s % runs); };
     // A stable sort of each queue's slots (s = f*runs + r, ascending) by cost[r], longest first, in
     // O(slots): the runs by (cost descending, r ascending) once; a queue then takes each group of
     // equal-cost runs frame by frame (ascending slot order within a group is frame-major).
@@ -198,7 +223,7 @@ void build_item_table(const std::vector<float> &cost, unsigned bandPixels, unsig
     for (unsigned g = 0; g < queues && s0 < slots; ++g) {
         const unsigned long long end = total * (g + 1) / queues;
         size_t s1 = s0;
-        while (s1 < slots && item(s1) < end) ++s1;  // the queue's slots [s0, s1)
+        while (s1 < slots && pos(s1) < end) ++s1;  // the queue's slots [s0, s1)
         if (s1 == s0) continue;
         const size_t f0 = s0 / runs, f1 = (s1 - 1) / runs;
         size_t out = s0;

@@ -55,6 +55,7 @@ OPT_ITEM_ORDER = 28
 OPT_WAVEFRONT_SORT = 29
 OPT_CHAIN = 30
 OPT_CHAIN_AUDIT = 31
+OPT_PIXEL_TILE = 32
 OPT_PIXEL_FORMAT = 25
 PIXEL_ARGB = 0
 PIXEL_RGBA8 = 1

@@ -505,6 +505,41 @@ def test_camera_pool_does_not_change_results(pt, name, variant):
         pt.resetStats()
 
 
+@pytest.mark.parametrize("tile", [0, 8, 16, 32])
+@pytest.mark.parametrize("name,w,h,frames", [("cornell34", 192, 77, 3), ("blob70k", 131, 64, 2),
+                                               ("blob70k", 160, 45, 2), ("cornell_mixed", 96, 53, 2)])
+def test_item_order_tiles(pt, name, w, h, frames, tile):
+    """HIPPT_OPT_PIXEL_TILE: the item order's runs as tiles of `tile` columns x 64 / tile band rows
+    over the band's whole strips, then row runs (item_order.h RunLayout; a width that is not a
+    multiple of the tile keeps row runs).  Blocking and chained async batches, the whole image and an
+    interleaved row share: the oracle's images and counts."""
+    sc = scenes.get_scene(name)
+    ora = po.MeshScene(sc, w, h).frames(0, frames, 8)
+    pt.uploadMesh(sc)
+    pt.setOption(hippt.OPT_PIXEL_TILE, tile)
+    try:
+        assert pt.initialize(w, h), pt.lastError()
+        assert pt.renderFrames(frames, 8), pt.lastError()
+        got = pt.readback()
+        _assert_same(got[0], got[1], ora[0], ora[1])
+        st = pt.stats()
+        assert st["segments"] == ora[2] and st["pixelSamples"] == ora[3]
+        assert pt.initialize(w, h)
+        for _ in range(frames):
+            assert pt.renderFramesAsync(1, 8), pt.lastError()
+        got = pt.readback()
+        _assert_same(got[0], got[1], ora[0], ora[1])
+        pt.setRowInterleave(1, 3)
+        assert pt.initialize(w, h)
+        assert pt.renderFrames(frames, 8)
+        got = pt.readback()
+        rows = np.arange(1, h, 3)
+        _assert_same(got[0][rows], got[1][rows], ora[0][rows], ora[1][rows])
+    finally:
+        pt.setRowRange(0, 0)
+        pt.setOption(hippt.OPT_PIXEL_TILE, -1)
+
+
 @pytest.mark.parametrize("name,w,h,frames", [("cornell34", 200, 77, 3), ("blob70k", 131, 64, 2),
                                                ("cornell_mixed", 96, 53, 2)])
 def test_item_order_does_not_change_results(pt, name, w, h, frames):
