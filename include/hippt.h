@@ -265,7 +265,8 @@ enum {
     , HIPPT_OPT_PIXEL_TILE = 32     /* the item order's (HIPPT_OPT_ITEM_ORDER) unit of 64 pixels: tiles of this
                                        many columns x 64 / it band rows (8, 16 or 32; the image width a
                                        multiple of it), or 64 consecutive pixels of a row (0); -1 (default):
-                                       automatic.  Same results either way */
+                                       automatic (8 for a band of consecutive rows, 0 for interleaved row
+                                       shares).  Same results either way */
 };
 /* Records of the chained runs closed since the last call (HIPPT_OPT_CHAIN_AUDIT), as 32-bit words:
  * per run a 16-word header  [0] 0xC4A1D17 [1] run id [2] device [3] batch 0's first frame [4] frames

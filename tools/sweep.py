@@ -30,7 +30,7 @@ KEYS = {"wave": hippt.OPT_WAVE_THRESHOLD, "chunk": hippt.OPT_CHUNK, "scratch": h
         "quant": hippt.OPT_BVH_QUANT, "top": hippt.OPT_LDS_TOP_NODES,
         "collapse": hippt.OPT_BVH_COLLAPSE, "ncost": hippt.OPT_BVH_NODE_COST, "leaf4": hippt.OPT_BVH_LEAF4,
         "rngtab": hippt.OPT_RNG_TABLE, "pool": hippt.OPT_CAMERA_POOL, "fuse": hippt.OPT_FUSE_COMBINE,
-        "order": hippt.OPT_ITEM_ORDER}
+        "order": hippt.OPT_ITEM_ORDER, "tile": hippt.OPT_PIXEL_TILE, "chain": hippt.OPT_CHAIN}
 REUPLOAD = {"leaf", "tcost", "depth", "sah", "collapse", "ncost", "leaf4"}  # build parameters: take effect at the next upload
 
 
