@@ -205,7 +205,8 @@ struct Ctx {
         bool closed;
     };
     std::vector<AuditRun> auditRuns;
-    hipEvent_t chainStartEv = nullptr;  // recorded before each chained launch (chain_batch's skip test)
+    hipEvent_t chainStartEv = nullptr;  // recorded before each chained launch (chain_batch's hold test)
+    hipEvent_t chainEndEv = nullptr;    // recorded after each chained launch (chain_batch's hold test)
     unsigned *chainCtl = nullptr;
     float *chainScratch = nullptr;
     size_t chainScratchBytes = 0;
@@ -463,6 +464,7 @@ void destroy_ctx(Ctx &c) {
     (void)hipFree(c.chainScratch);
     if (c.chainBox) (void)hipHostFree(c.chainBox);
     if (c.chainStartEv) (void)hipEventDestroy(c.chainStartEv);
+    if (c.chainEndEv) (void)hipEventDestroy(c.chainEndEv);
     (void)hipFree(c.stats);
     (void)hipFree(c.wfPool);
     (void)hipFree(c.wfCtr);
@@ -1103,6 +1105,11 @@ bool chain_auto(unsigned total, bool ldsScene, bool full) { return total <= (1u 
 #define HIPPT_CHAIN_GROUPS 1
 #endif
 constexpr bool kChainGroups = HIPPT_CHAIN_GROUPS != 0;
+// chain_batch holds the batches that arrive while the run's first launch runs (an A/B build knob)
+#ifndef HIPPT_CHAIN_HOLD_RUNNING
+#define HIPPT_CHAIN_HOLD_RUNNING 1
+#endif
+constexpr bool kChainHoldRunning = HIPPT_CHAIN_HOLD_RUNNING != 0;
 
 unsigned chain_cap(long long option, unsigned total) {
     if (option > 0) return unsigned(std::min<long long>(option, 8));
@@ -1201,12 +1208,14 @@ bool launch_chained(Ctx &c, hippt::MeshParams &p, const char **err) {
     ch.lastOwn = p.chainSeq;
     ch.pendN = 0;
     if (!c.chainStartEv) HIP_TRY(hipEventCreateWithFlags(&c.chainStartEv, hipEventDisableTiming));
+    if (!c.chainEndEv) HIP_TRY(hipEventCreateWithFlags(&c.chainEndEv, hipEventDisableTiming));
     EventPair ev;
     if (!next_events(c, ev, err)) return false;
     HIP_TRY(hipEventRecord(c.chainStartEv, c.stream));
     HIP_TRY(hipEventRecord(ev.a, c.stream));
     HIP_TRY(hippt::launch_mesh(p, int(ch.blocks), false, c.stream));
     HIP_TRY(hipEventRecord(ev.b, c.stream));
+    HIP_TRY(hipEventRecord(c.chainEndEv, c.stream));
     c.pending.push_back({0, ev});
     return true;
 }
@@ -1338,8 +1347,12 @@ bool chain_batch(Ctx &c, hippt::MeshParams &p, long long blocks, const RingPlan 
     const unsigned seq = ch.seq++;
     // held while the last launch has not started and the group is not full (64-item runs only: the
     // group interleaves its batches' runs)
+    // (kChainHoldRunning: also while the run's only launch so far is still running — the burst's
+    // second batch then opens the first group instead of being taken by that launch on its own walk
+    // of the item order and leaving its own launch nothing but the combine)
     const bool hold = kChainGroups && ch.epoch > 0 && ch.pendN + 1u < ch.cap && p.totalItems % 64u == 0 &&
-                      hipEventQuery(c.chainStartEv) == hipErrorNotReady;
+                      (hipEventQuery(c.chainStartEv) == hipErrorNotReady ||
+                       (kChainHoldRunning && ch.epoch == 1 && hipEventQuery(c.chainEndEv) == hipErrorNotReady));
 #ifdef HIPPT_CHAIN_TRACE
     std::fprintf(stderr, "chain run %u seq %u %s (held %u epoch %u cap %u slots %u)\n", ch.run, seq,
                  hold ? "held" : ch.pendN ? "launched with the held ones" : "launched", ch.pendN, ch.epoch,

@@ -140,6 +140,7 @@ struct Model {
     // configuration
     unsigned cap, slots, blocks, wavesPerBlock, units, chunk;
     double hostRate, retryRate, leaveRate;
+    bool holdRunning;
     // time
     unsigned long long now = 1000000;
     // host
@@ -195,6 +196,7 @@ struct Model {
         leaveRate = leaves[rng.below(3)];
         wavesPerBlock = 1 + rng.below(4);
         chunk = 1u << rng.below(3);
+        holdRunning = rng.chance(0.5);
         markers.assign(16, 0);
         counter.assign(16, 0);
         scratch.assign(16, std::vector<Slot>(64));
@@ -209,6 +211,10 @@ struct Model {
 
     // ---- host: chain_batch / flush_chain (hippt_api.cpp) ------------------------------------------
     bool lastLaunchStarted() const { return H.lastLaunch < 0 || stream[size_t(H.lastLaunch)].started; }
+    // the run's last launch has ended: the device is past it in the stream
+    bool lastLaunchFinished() const {
+        return H.lastLaunch < 0 || head > size_t(H.lastLaunch);
+    }
     void enqueueLaunch(Item p) {
         p.epoch = H.epoch++;
         H.pendN = 0;
@@ -274,7 +280,10 @@ struct Model {
         truth[{H.run, H.seq}] = ff;
         traced[{H.run, H.seq}] = std::vector<int>(units, 0);
         const unsigned seq = H.seq++;
-        const bool hold = H.epoch > 0 && H.pendN + 1u < cap && !lastLaunchStarted();
+        // hippt_api.cpp chain_batch: held while the run's last launch has not started, and (kChainHoldRunning)
+        // while the run's only launch so far still runs
+        const bool hold = H.epoch > 0 && H.pendN + 1u < cap &&
+                          (!lastLaunchStarted() || (holdRunning && H.epoch == 1 && !lastLaunchFinished()));
         if (hold) {
             if (!H.pendN) H.pendP = p;
             ++H.pendN;
