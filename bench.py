@@ -144,7 +144,16 @@ def host_cpu_facts() -> dict:
     except (AttributeError, OSError):
         affinity = os.cpu_count() or 1
     omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
-    return {"nproc": os.cpu_count(), "affinity": affinity, "omp_num_threads": omp or None, "model": model}
+    # the cgroup's CPU bandwidth limit (cgroup v2 cpu.max: "quota period" or "max period"), in cores
+    quota = None
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+            quota = None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    return {"nproc": os.cpu_count(), "affinity": affinity, "omp_num_threads": omp or None, "model": model,
+            "cgroup_cpu_quota_cores": quota}
 
 
 def cpu_threads(args, facts) -> tuple[int, str]:
@@ -221,10 +230,13 @@ def cpu_baseline(args, scene) -> dict | None:
             eff = r["msamples_per_s"] / (threads * one["msamples_per_s"])
             out["per_thread"] = {"value": round(one["msamples_per_s"], 4), "threads": 1,
                                  "parallel_efficiency_at_cores": round(eff, 3)}
-            out["full_affinity_projected"] = {
-                "value": round(one["msamples_per_s"] * facts["affinity"] * eff, 2), "threads": facts["affinity"],
-                "rule": "1-thread rate x affinity-mask threads x the measured parallel efficiency at `cores` "
-                        "threads (projected: the box's CPU share is `cores`; not timed at the mask's size)"}
+            # the reference's tile pool is embarrassingly parallel (RayTracerFboItem.cpp:75-90), so the
+            # whole mask's rate is at most the 1-thread rate times its threads; a box whose cgroup
+            # quota caps the share shows it as a parallel efficiency far below 1 at `cores` threads
+            out["full_affinity_upper_bound"] = {
+                "value": round(one["msamples_per_s"] * facts["affinity"], 2), "threads": facts["affinity"],
+                "rule": "1-thread rate x affinity-mask threads (linear scaling, an upper bound: not timed at the "
+                        "mask's size, which the box's CPU share does not allow)"}
         return out
     ms = pyoracle.MeshScene(scene, args.width, args.height, accel=1)
     t0 = time.perf_counter()
