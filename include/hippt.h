@@ -251,11 +251,11 @@ enum {
                                        batches with the same scene, camera, rows and frames per batch (each
                                        the same frames again or the next ones) form a run, and a launch whose
                                        batch is drained goes on with the batches posted behind it, up to this
-                                       many (1..8), so that the run pays the launch's tail once per that many
+                                       many (1..16), so that the run pays the launch's tail once per that many
                                        batches; the next launch combines them beside its own paths and the
                                        image's readers flush the rest.  0: one launch per batch; -1
                                        (default): automatic (on for batches of at most 2^26 samples, for
-                                       trees in global memory and for the general kernel; 2..8 batches by
+                                       trees in global memory and for the general kernel; 2..16 batches (8 over LDS-resident scenes) by
                                        the batch's size).  Same results either way */
     , HIPPT_OPT_CHAIN_AUDIT = 31    /* 1: chained launches record, per batch of each run, the work items they
                                        traced (count and a hash of their indices), the frames and the launch

@@ -1111,10 +1111,16 @@ constexpr bool kChainGroups = HIPPT_CHAIN_GROUPS != 0;
 #endif
 constexpr bool kChainHoldRunning = HIPPT_CHAIN_HOLD_RUNNING != 0;
 
-unsigned chain_cap(long long option, unsigned total) {
-    if (option > 0) return unsigned(std::min<long long>(option, 8));
+// The automatic cap's ceiling: 16 for trees in global memory, 8 for LDS-resident scenes.  A bigger
+// cap makes a burst's groups bigger (a 1/8 row share's 20 steps: 3 launches instead of 4), and the
+// launch after a group combines the whole group: hidden behind a global tree's slower batches
+// (blob70k 1/8 share 2.538/2.539 -> 2.497/2.493 ms, 1/4 share 4.799/4.778 -> 4.754/4.754), exposed
+// beside Cornell's (1/8 share 0.991/0.989 -> 1.025/1.015: the last launch's 16-batch combine adds
+// ~0.9 ms), r6n.
+unsigned chain_cap(long long option, unsigned total, bool ldsScene) {
+    if (option > 0) return unsigned(std::min<long long>(option, 16));
     const double c = std::round(4e8 / double(std::max(1u, total)));
-    return unsigned(std::clamp(c, 2.0, 8.0));
+    return unsigned(std::clamp(c, 2.0, ldsScene ? 8.0 : 16.0));
 }
 
 // The ring of a run of `total`-item batches: 2^shift samples per slot (the slot bits above them in
@@ -1127,12 +1133,12 @@ struct RingPlan {
     unsigned cap = 0, slots = 0, shift = 0;
     size_t bytes = 0;
 };
-RingPlan ring_plan(unsigned total, long long option, size_t budget) {
+RingPlan ring_plan(unsigned total, long long option, bool ldsScene, size_t budget) {
     RingPlan r;
     r.shift = 6;
     while ((1u << r.shift) < total) ++r.shift;
     const size_t slotBytes = (size_t(1) << r.shift) * 3 * sizeof(float);
-    for (unsigned cap = chain_cap(option, total); cap >= 1; --cap) {
+    for (unsigned cap = chain_cap(option, total, ldsScene); cap >= 1; --cap) {
         unsigned slots = 2;
         while (slots < 2 * cap) slots <<= 1;
         slots = std::min(slots, hippt::kChainSlotsMax);
@@ -1548,7 +1554,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                                    total <= (1u << hippt::kChainMaxShift);
                     RingPlan ring;
                     if (chained) {
-                        ring = ring_plan(total, s.chainBatches, cap);
+                        ring = ring_plan(total, s.chainBatches, ldsScene, cap);
                         bool ok = ring.bytes != 0;
                         if (ok && !ensure_ring(c, ring, &ok, err)) return false;
                         chained = ok;
@@ -2416,7 +2422,7 @@ extern "C" bool hipptSetOption(int key, long long value) try {
         s.wfSort = int(value);
         return true;
     case HIPPT_OPT_CHAIN:
-        if (value < -1 || value > 8) return false;
+        if (value < -1 || value > 16) return false;
         s.chainBatches = int(value);
         return true;
     case HIPPT_OPT_CHAIN_AUDIT:

@@ -144,7 +144,7 @@ struct MeshParams {
 // the last launch that took a batch in this slot.  After the kChainSlotsMax blocks, at kChainCtlWord:
 // the first batch not yet combined after the launches of epoch parity 0 / 1 (+0 / +32), the combine
 // chunk counters of epoch parity 0 / 1 (+64 / +96).
-constexpr unsigned kChainSlotsMax = 16, kChainBlockWords = 8 * 32 + 32, kChainMarkerWord = 8 * 32;
+constexpr unsigned kChainSlotsMax = 32, kChainBlockWords = 8 * 32 + 32, kChainMarkerWord = 8 * 32;
 constexpr unsigned kChainCtlWord = kChainSlotsMax * kChainBlockWords;
 // (+128: kQueues device copies of the host mailbox, one 128-byte line each, for the blocks of one
 // XCD: the copy (64-bit), the realtime stamp of its last completed refresh, the stamp of the last

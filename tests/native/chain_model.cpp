@@ -182,10 +182,10 @@ struct Model {
     long stats[4] = {0, 0, 0, 0};  // closed merges, answers from a closed view, takes from one
 
     Model(const Rules &r, uint64_t seed, Violations &v) : R(r), rng(seed), V(v) {
-        cap = 1 + rng.below(8);
+        cap = 1 + rng.below(rng.chance(0.25) ? 16 : 8);
         slots = 2;
         while (slots < (&R == &kSmallRing ? cap : 2 * cap)) slots <<= 1;
-        if (slots > 16) slots = 16;
+        if (slots > 32) slots = 32;
         blocks = 1 + rng.below(4);
         wavesPerBlock = 1 + rng.below(3);
         units = 1 + rng.below(12);
@@ -197,9 +197,9 @@ struct Model {
         wavesPerBlock = 1 + rng.below(4);
         chunk = 1u << rng.below(3);
         holdRunning = rng.chance(0.5);
-        markers.assign(16, 0);
-        counter.assign(16, 0);
-        scratch.assign(16, std::vector<Slot>(64));
+        markers.assign(32, 0);
+        counter.assign(32, 0);
+        scratch.assign(32, std::vector<Slot>(256));
     }
 
     std::string where() const {
