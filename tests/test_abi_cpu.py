@@ -96,7 +96,9 @@ def test_options_validate():
     (hippt.OPT_STACK_CAP, (0, 4, 30), (3, 31), 0),
     (hippt.OPT_BVH_QUANT, (-1, 0, 1, 2, 3), (-2, 4), -1),
     (hippt.OPT_WAVEFRONT_SORT, (-1, 0, 3, 6), (-2, 1, 2, 4, 7), -1),
-    (hippt.OPT_CHAIN, (-1, 0, 1, 2, 8), (-2, 9), -1),
+    (hippt.OPT_CHAIN, (-1, 0, 1, 2, 8, 16), (-2, 17), -1),
+    (hippt.OPT_CHAIN_AUDIT, (0, 1), (-1, 2), 0),
+    (hippt.OPT_PIXEL_TILE, (-1, 0, 8, 16, 32), (-2, 4, 12, 64), -1),
 ])
 def test_round2_options_round_trip(key, good, bad, default):
     """Each option accepts its documented range (include/hippt.h), reads back what was set,
