@@ -90,6 +90,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--prewarm-ms", type=float, default=200.0,
+                   help="untimed GPU clock warm-up before the warmup steps: whole steps for this many ms")
     p.add_argument("--scene", default="cornell34",
                    choices=["cornell34", "blob70k", "random_scene", "cornell_mixed"])
     p.add_argument("--path-mode", default="megakernel", choices=["megakernel", "wavefront"],
@@ -484,6 +486,18 @@ def main():
     bvh_width = pt._lib.hipptActiveBvhWidth()  # the tree nodeVisits count (2- or 4-wide)
     pt.setOption(hippt.OPT_COUNT_TRAVERSAL, 0)
 
+    # GPU clock warm-up (untimed, before the W warmup steps): the first ~20 ms of GPU work after an
+    # idle period run slow (the whole image's first three launches 7.69 / 7.49 / 7.17 ms, then
+    # 7.14–7.16; a 1/8 share's first 4-batch groups 4.10 / 4.05 / 3.91 / 3.84 ms, then 3.73–3.76:
+    # DESIGN_LOG.md §A.R6, r6q), which W steps of a 1/N share (W ms at N = 8) do not cover.  Every
+    # rank, at every N, runs whole steps until --prewarm-ms of wall time have passed.
+    t_warm = time.perf_counter()
+    prewarm_steps = 0
+    while (time.perf_counter() - t_warm) * 1e3 < args.prewarm_ms:
+        step()
+        prewarm_steps += 1
+        if prewarm_steps % 4 == 0:
+            device_sync(pt)
     for _ in range(args.warmup):
         step()
     device_sync(pt)
@@ -552,6 +566,7 @@ def main():
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
+            "prewarm": {"ms": args.prewarm_ms, "steps": prewarm_steps},
             "ms_per_step": round(elapsed_max * 1e3 / args.steps, 4),
             "higher_is_better": True,
             "scaling": args.scaling,

@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--ranks", default="1,2,4,8")
     ap.add_argument("--all-bands", action="store_true", help="time every rank's rows (max = the N-GPU step)")
     ap.add_argument("--split", default="interleave", choices=["interleave", "bands"])
+    ap.add_argument("--prewarm-ms", type=float, default=200.0, help="untimed GPU clock warm-up per job")
     ap.add_argument("opts", nargs="*", help="KEY=VALUE hipptSetOption pairs (numeric keys)")
     a = ap.parse_args()
     sc = scenes.get_scene(a.scene)
@@ -49,7 +50,13 @@ def main():
         pt.uploadMesh(sc)
         assert pt.initialize(a.width, a.height)
         lib = pt._lib
+        # clock warm-up (as bench.py --prewarm-ms): whole steps for a.prewarm_ms of wall time
+        t_warm = time.perf_counter()
         lib.hipptRenderFramesAsync(0, a.spp, a.depth, None)
+        while (time.perf_counter() - t_warm) * 1e3 < a.prewarm_ms:
+            for _ in range(4):
+                lib.hipptRenderFramesAsync(0, a.spp, a.depth, None)
+            pt.synchronize()
         pt.synchronize()
         pt.resetStats()
         t0 = time.perf_counter()
