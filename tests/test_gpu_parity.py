@@ -578,6 +578,7 @@ def test_item_order_camera_change_does_not_stall(pt):
     import time
     sc = scenes.cornell34()
     w, h = 1920, 1080
+    pt.setOption(hippt.OPT_ITEM_ORDER, -1)  # the automatic mode under test (the fixture forces 1)
     pt.uploadMesh(sc)
     assert pt.initialize(w, h), pt.lastError()
     assert pt.renderFrames(1, 8, copy=False), pt.lastError()
