@@ -689,7 +689,7 @@ def test_mesh_batches_and_frame_splits_are_bit_identical(pt):
     _assert_same(one[0], one[1], split[0], split[1])
 
 
-@pytest.mark.parametrize("order", [0, 1])
+@pytest.mark.parametrize("order", [0, 1, -1])
 @pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene", "cornell_mixed"])
 def test_chained_batches_match_oracle(pt, name, order):
     """HIPPT_OPT_CHAIN (Ctx::chain, hippt_trace.h chained batches): a launch whose batch is drained
@@ -946,13 +946,15 @@ def test_chain_ring_within_scratch_budget(pt):
     pt.setOption(hippt.OPT_SCRATCH_MB, 32768)
 
 
-@pytest.mark.parametrize("order", [0, 1])
+@pytest.mark.parametrize("order", [0, 1, -1])
 @pytest.mark.parametrize("name", ["cornell34", "blob70k", "random_scene"])
 def test_deferred_combine_across_async_calls(pt, name, order):
     """Back-to-back hipptRenderFramesAsync calls: each megakernel batch's combine (running average
     + tonemap) runs inside the next batch's launch (Ctx::deferred), from the other scratch buffer;
     anything that reads or resets the image runs the pending one first.  Every sequence below
-    gives the oracle's progressive image bit for bit."""
+    gives the oracle's progressive image bit for bit.  Item order 0 and 1 fix the code path; -1
+    (the library's default) lets the detached cost job finish at any point of a sequence, closing
+    the chained run it lands in (GPUTEST_r05's trigger) — exact and audited all the same."""
     sc = scenes.get_scene(name)
     w, h = 45, 26
     ora6 = po.MeshScene(sc, w, h).frames(0, 6, 8)
