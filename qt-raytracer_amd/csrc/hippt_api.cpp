@@ -1125,7 +1125,7 @@ unsigned chain_cap(long long option, unsigned total, bool ldsScene) {
 
 // The ring of a run of `total`-item batches: 2^shift samples per slot (the slot bits above them in
 // an item), at least 2 x cap slots (a launch traces up to cap batches while up to cap batches before
-// its own wait for its combine), 12 bytes per sample (kRadFloats).  The ring stays within the sample-scratch
+// its own wait for its combine), 12 bytes per sample.  The ring stays within the sample-scratch
 // budget (HIPPT_OPT_SCRATCH_MB): the cap shrinks until it fits, and a batch whose smallest ring
 // (2 slots) does not fit runs unchained (bytes = 0).  (blob70k at 1080p/64 spp and cap 8
 // asked for 25.8 GB whatever the budget.)
@@ -1137,7 +1137,7 @@ RingPlan ring_plan(unsigned total, long long option, bool ldsScene, size_t budge
     RingPlan r;
     r.shift = 6;
     while ((1u << r.shift) < total) ++r.shift;
-    const size_t slotBytes = (size_t(1) << r.shift) * hippt::kRadFloats * sizeof(float);
+    const size_t slotBytes = (size_t(1) << r.shift) * 3 * sizeof(float);
     for (unsigned cap = chain_cap(option, total, ldsScene); cap >= 1; --cap) {
         unsigned slots = 2;
         while (slots < 2 * cap) slots <<= 1;
@@ -1427,7 +1427,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                 c.pending.push_back({0, ev});
             } else {
                 if (!ensure_scene(c, err)) return false;
-                const size_t perFrame = size_t(bandPixels) * hippt::kRadFloats * sizeof(float);
+                const size_t perFrame = size_t(bandPixels) * 3 * sizeof(float);
                 const size_t cap = size_t(std::max<long long>(1, s.scratchMB)) << 20;
                 int fpb = int(std::max<size_t>(1, cap / perFrame));
                 fpb = std::min(fpb, count);
@@ -1565,7 +1565,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                     if (!chained && !batch_scratch(c, need, &scratch, err)) return false;
                     if (maxDepth <= 0) {
                         // ray_color with depth <= 0 returns black without tracing (RayTracer.h:582-583)
-                        HIP_TRY(hipMemsetAsync(scratch, 0, size_t(total) * hippt::kRadFloats * sizeof(float), c.stream));
+                        HIP_TRY(hipMemsetAsync(scratch, 0, size_t(total) * 3 * sizeof(float), c.stream));
                     } else {
                         hippt::MeshParams p{};
                         p.nodes = hybrid ? c.nodes4h : quant ? c.nodes4q : half ? c.nodes4f : wide ? c.nodes4 : c.nodes;

@@ -25,14 +25,6 @@ struct Sphere4Params {
     uint32_t *hostOut;  // null, or the W*H full frame in pinned host memory (device-mapped)
 };
 
-// Floats per sample in the radiance scratch: 3 (one 12-byte store), or 4 (one aligned 16-byte
-// store, an A/B build knob for the partial-line write-back question, DESIGN_LOG.md §A.R6).
-#ifndef HIPPT_RAD_FLOATS
-#define HIPPT_RAD_FLOATS 3
-#endif
-constexpr unsigned kRadFloats = HIPPT_RAD_FLOATS;
-static_assert(kRadFloats == 3 || kRadFloats == 4, "HIPPT_RAD_FLOATS is 3 or 4");
-
 // Pixel word formats of the output frame (HIPPT_OPT_PIXEL_FORMAT)
 enum { kPixelArgb = 0, kPixelRgba8 = 1 };
 

@@ -224,15 +224,6 @@ __device__ unsigned long long g_rate[kRateSlots * kRateBuckets * 5];
 #ifndef HIPPT_WIDE_WAVES_PER_EU
 #define HIPPT_WIDE_WAVES_PER_EU 7
 #endif
-// One sample's radiance from the scratch (store_radiance's layout).
-__device__ __forceinline__ float3 load_radiance(const float *s) {
-    if constexpr (kRadFloats == 4) {
-        const float4 v = *reinterpret_cast<const float4 *>(s);
-        return make_float3(v.x, v.y, v.z);
-    }
-    return *reinterpret_cast<const float3 *>(s);
-}
-
 // Running average in frame order, then the output word (CudaPathTracerKernel.cu:157-178), of band
 // pixel p over a batch of per-sample radiances.
 template <int UNROLL, bool HOST = false>
@@ -243,7 +234,7 @@ __device__ __forceinline__ void combine_pixel(const CombineParams &P, unsigned p
         const size_t k = size_t(fl) * P.bandPixels + p;
         const int f = P.firstFrame + fl;
         const float ff = float(f), fc = float(f + 1);
-        const float3 L = load_radiance(P.scratch + kRadFloats * k);
+        const float3 L = *reinterpret_cast<const float3 *>(P.scratch + 3 * k);
         acc.x = fmaf(acc.x, ff, L.x) / fc;
         acc.y = fmaf(acc.y, ff, L.y) / fc;
         acc.z = fmaf(acc.z, ff, L.z) / fc;
@@ -280,11 +271,11 @@ __device__ __forceinline__ void combine_pixel_chain(const CombineParams &C, cons
                                                     const HostFrame &H = HostFrame{}) {
     float4 acc = C.accum[p];
     for (int b = c0; b <= c1; ++b) {
-        const float *scr = scratch + kRadFloats * ((size_t(unsigned(b) & (slots - 1u)) << shift) + p);
+        const float *scr = scratch + 3 * ((size_t(unsigned(b) & (slots - 1u)) << shift) + p);
         const int f0 = C.firstFrame + b * step;
 #pragma unroll UNROLL
         for (int fl = 0; fl < C.frames; ++fl) {
-            const float3 L = load_radiance(scr + kRadFloats * size_t(fl) * C.bandPixels);
+            const float3 L = *reinterpret_cast<const float3 *>(scr + 3 * size_t(fl) * C.bandPixels);
             const float ff = float(f0 + fl), fc = float(f0 + fl + 1);
             acc.x = fmaf(acc.x, ff, L.x) / fc;
             acc.y = fmaf(acc.y, ff, L.y) / fc;

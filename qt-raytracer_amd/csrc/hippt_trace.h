@@ -697,10 +697,7 @@ __device__ __forceinline__ void camera_sample(const PP &P, unsigned it, Ray &r, 
 // cost three, and the store instructions of lanes finishing at different times dominated the
 // address unit's load on LDS-resident scenes).
 __device__ __forceinline__ void store_radiance(float *scratch, unsigned item, float r, float g, float b) {
-    if constexpr (kRadFloats == 4)
-        *reinterpret_cast<float4 *>(scratch + 4 * size_t(item)) = make_float4(r, g, b, 0.0f);
-    else
-        *reinterpret_cast<float3 *>(scratch + 3 * size_t(item)) = make_float3(r, g, b);
+    *reinterpret_cast<float3 *>(scratch + 3 * size_t(item)) = make_float3(r, g, b);
 }
 
 // Sky gradient on a miss (RayTracer.h:593-595), times throughput; `inv` = 1/sqrtf(|d|^2).
