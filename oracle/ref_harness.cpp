@@ -421,10 +421,15 @@ int choose_tile(int w, int h) {
 
 // RenderWorker::render (RayTracerFboItem.cpp:46-144) without Qt; timing only.
 // Renders every `stride`-th line of a W x H image (a bounded, representative sample of
-// the workload: lines 0, stride, 2*stride, ...), tiled over the compacted lines.
-int cmd_bench(const char *scene_path, int W, int H, int stride, int spp, int depth, int threads) {
+// the workload: lines 0, stride, 2*stride, ...), tiled over the compacted lines.  With
+// `parts` > 1 only the sample's lines k with k % parts == part (one of `parts` processes
+// splitting the same sample).
+int cmd_bench(const char *scene_path, int W, int H, int stride, int spp, int depth, int threads, int part = 0,
+              int parts = 1) {
     if (stride < 1) stride = 1;
-    const int rows = (H + stride - 1) / stride;
+    if (parts < 1 || part < 0 || part >= parts) parts = 1, part = 0;
+    const int sampleRows = (H + stride - 1) / stride;
+    const int rows = sampleRows > part ? (sampleRows - part + parts - 1) / parts : 0;
     Scene s;
     if (!load_scene(scene_path, s)) return 3;
     auto t_setup = std::chrono::steady_clock::now();
@@ -454,7 +459,7 @@ int cmd_bench(const char *scene_path, int W, int H, int stride, int spp, int dep
                 int x0 = (idx % tilesX) * tile, y0 = (idx / tilesX) * tile;
                 int x1 = std::min(x0 + tile, W), y1 = std::min(y0 + tile, rows);
                 for (int line = y0; line < y1; ++line) {
-                    const int j = H - 1 - line * stride;
+                    const int j = H - 1 - (part + line * parts) * stride;
                     for (int i = x0; i < x1; ++i) {
                         Color pc(0, 0, 0);
                         for (int k = 0; k < spp; ++k) {
@@ -498,11 +503,12 @@ int main(int argc, char **argv) {
     if (argc >= 3 && std::strcmp(argv[1], "random_scene") == 0) return cmd_random_scene(argv[2]);
     if (argc >= 8 && std::strcmp(argv[1], "bench") == 0)
         return cmd_bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), std::atoi(argv[5]), std::atoi(argv[6]),
-                         std::atoi(argv[7]), argc >= 9 ? std::atoi(argv[8]) : 0);
+                         std::atoi(argv[7]), argc >= 9 ? std::atoi(argv[8]) : 0, argc >= 10 ? std::atoi(argv[9]) : 0,
+                         argc >= 11 ? std::atoi(argv[10]) : 1);
     std::fprintf(stderr,
                  "usage: ref_harness golden OUT.json [SCENE]\n"
                  "       ref_harness converge SCENE W H SPP DEPTH OUT.f32 [THREADS]\n"
-                 "       ref_harness bench SCENE W H STRIDE SPP DEPTH [THREADS]\n"
+                 "       ref_harness bench SCENE W H STRIDE SPP DEPTH [THREADS [PART PARTS]]\n"
                  "       ref_harness random_scene OUT.scene\n");
     return 1;
 }
