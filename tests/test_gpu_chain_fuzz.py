@@ -6,6 +6,7 @@ image and accumulation equal the same sequence with one launch per batch (HIPPT_
 checked against the oracle by test_gpu_parity.py), and the device audit of every chained run is
 clean (each batch traced once with its own frames, combined once, in order)."""
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -66,7 +67,7 @@ def _ops(rng):
         r = rng.random()
         if r < 0.5:
             ops.append(("next", pick()))
-        elif r < 0.66:
+        elif r < 0.60:
             ops.append(("again", pick()))
         elif r < 0.66:
             ops.append(("jump", int(rng.integers(1, 5))))
@@ -83,7 +84,8 @@ def _ops(rng):
     return ops
 
 
-@pytest.mark.parametrize("seed", range(16))
+# HIPPT_FUZZ_SEEDS widens the run (the suite's default is 16 sequences; profiles/round6 logs a longer one)
+@pytest.mark.parametrize("seed", range(int(os.environ.get("HIPPT_FUZZ_SEEDS", "16"))))
 def test_random_chained_sequences_equal_one_launch_per_batch(seed):
     rng = np.random.default_rng(1000 + seed)
     pt = hippt.PathTracer()
