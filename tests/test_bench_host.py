@@ -70,6 +70,29 @@ def test_missing_reference_harness_is_reported_not_substituted(bench, monkeypatc
     assert cb["value"] is None and cb["kind"] == "reference" and "missing" in cb["error"]
 
 
+def test_reference_harness_parts_cover_the_sample(tmp_path):
+    """cpu_baseline's independent_processes: `ref_harness bench ... 1 PART PARTS` renders the sample
+    lines k with k % PARTS == PART, so the parts' lines and pixel samples add up to the whole sample."""
+    import json
+    import subprocess
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pyoracle
+    from hippt import scenes
+    if not os.path.exists(pyoracle.REF_HARNESS):
+        pytest.skip("oracle/_ref/ref_harness not built (needs /root/reference)")
+    path = str(tmp_path / "c.scene")
+    scenes.write_scene_file(scenes.get_scene("cornell34"), path)
+
+    def run(*extra):
+        out = subprocess.run([pyoracle.REF_HARNESS, "bench", path, "64", "37", "3", "1", "2", "1", *extra],
+                             capture_output=True, text=True, check=True, timeout=120).stdout
+        return json.loads(out.strip().splitlines()[-1])
+    whole = run()
+    parts = [run(str(k), "3") for k in range(3)]
+    assert whole["rows"] == 13 and [p["rows"] for p in parts] == [5, 4, 4]
+    assert sum(p["pixel_samples"] for p in parts) == whole["pixel_samples"]
+
+
 def test_pmc_summary_used_only_for_the_same_run(bench):
     """roofline.traffic comes from a PMC summary only when it describes this
     run — the same image CRC traced by the same libhippt.so (its SHA-256) — and carries bytes per
