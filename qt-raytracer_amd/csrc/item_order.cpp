@@ -219,13 +219,6 @@ void build_item_table(const std::vector<float> &cost, const RunLayout &L, unsign
     for (size_t k = 1; k < runs; ++k)
         if (cost[ranked[k]] != cost[ranked[k - 1]]) group.push_back(k);
     group.push_back(runs);
-#ifdef HIPPT_EXP_REGION_QUEUES
-    std::vector<size_t> rb0(runs), rbLen(runs);  // run r's band of runs: first run, length
-    for (unsigned b = 0; b < queues; ++b) {
-        const size_t a = runs * b / queues, e = runs * (b + 1) / queues;
-        for (size_t r = a; r < e; ++r) rb0[r] = a, rbLen[r] = e - a;
-    }
-#endif
     size_t s0 = 0;
     for (unsigned g = 0; g < queues && s0 < slots; ++g) {
         const unsigned long long end = total * (g + 1) / queues;
@@ -247,18 +240,6 @@ void build_item_table(const std::vector<float> &cost, const RunLayout &L, unsign
                         if (sl >= s0 && sl < s1) table[out++] = item(sl);
                     }
         }
-#elif defined(HIPPT_EXP_REGION_QUEUES)
-        // experiment: queue g's positions hold the items of the g-th band of runs (image order) over
-        // every frame instead of every run over its own frames, so that the waves of one XCD (the
-        // blocks b with b % queues == g) start their paths in one part of the image
-        (void)f0;
-        (void)f1;
-        for (size_t k = 0; k + 1 < group.size(); ++k)
-            for (size_t f = 0; f < frames; ++f)
-                for (size_t q = group[k]; q < group[k + 1]; ++q) {
-                    const size_t r = ranked[q], b0 = rb0[r], li = frames * b0 + f * rbLen[r] + (r - b0);
-                    if (li >= s0 && li < s1) table[out++] = item(f * runs + r);
-                }
 #else
         for (size_t k = 0; k + 1 < group.size(); ++k)
             for (size_t f = f0; f <= f1; ++f)
@@ -269,17 +250,7 @@ void build_item_table(const std::vector<float> &cost, const RunLayout &L, unsign
 #endif
         s0 = s1;
     }
-#ifdef HIPPT_EXP_REGION_QUEUES
-    for (; s0 < slots; ++s0) {  // positions past the last queue: the remaining region-major items
-        const size_t li = s0;
-        size_t b = 0;
-        while (b + 1 < queues && runs * (b + 1) / queues * frames <= li) ++b;
-        const size_t a = runs * b / queues, len = runs * (b + 1) / queues - a, off = li - frames * a;
-        table[s0] = item((off / len) * runs + a + off % len);
-    }
-#else
     for (; s0 < slots; ++s0) table[s0] = item(s0);
-#endif
 }
 
 }  // namespace hippt

@@ -48,10 +48,8 @@ static int check_table(unsigned width, unsigned rows, unsigned frames, unsigned 
     std::vector<uint32_t> t, ref;
     build_item_table(cost, L, frames, queues, t);
     if (t.size() != runs * frames) return 1;
-#ifndef HIPPT_EXP_REGION_QUEUES
     reference_table(cost, L, frames, queues, ref);
     if (t != ref) return 4;
-#endif
     // every (frame, band pixel) exactly once: the slots' 64 items each, then the positions past the
     // frame's whole runs as themselves (trace::order_item)
     std::vector<unsigned char> seen(size_t(bandPixels) * frames, 0);
