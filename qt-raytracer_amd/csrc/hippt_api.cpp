@@ -284,6 +284,16 @@ struct State {
     bool chainAudit = false;            // HIPPT_OPT_CHAIN_AUDIT
     std::vector<unsigned> auditWords;   // closed runs' audit words not yet read (hipptChainAudit)
     std::vector<std::pair<int, uint32_t *>> rngTables;  // per device, built on first use
+    // The big work buffers (sample scratch, chain ring, spill area) of the contexts a re-initialization
+    // destroyed, kept for the new contexts of the same device: a fresh hipMalloc of a 13 GB ring took
+    // up to 5.9 s and its hipFree ~0.29 s (r6ae/r6af), a stall on the first render after every resize.
+    // Held for one initialization; cudaPathTracerShutdown frees them.
+    struct SpareBuf {
+        int device;
+        void *ptr;
+        size_t bytes;
+    };
+    std::vector<SpareBuf> spare;
     unsigned activeTopBytes = 0;  // of the last mesh render (hipptGetOption HIPPT_INFO_*)
     int activeBlocksPerCu = 0;
     int activeChunk = 0;     // the last megakernel batch's claim size
@@ -305,6 +315,34 @@ struct State {
 State &S() {
     static State s;
     return s;
+}
+
+// A kept buffer of `device` of at least `need` bytes (the smallest such), or null.
+void *spare_take(int device, size_t need, size_t *bytes) {
+    auto &v = S().spare;
+    size_t best = v.size();
+    for (size_t k = 0; k < v.size(); ++k)
+        if (v[k].device == device && v[k].bytes >= need && (best == v.size() || v[k].bytes < v[best].bytes)) best = k;
+    if (best == v.size()) return nullptr;
+    void *p = v[best].ptr;
+    *bytes = v[best].bytes;
+    v.erase(v.begin() + long(best));
+    return p;
+}
+
+void spare_free_all() {
+    for (auto &b : S().spare) {
+        (void)hipSetDevice(b.device);
+        (void)hipFree(b.ptr);
+    }
+    S().spare.clear();
+}
+
+// hipMalloc of a big work buffer, or a kept one of the same device (spare_take); *bytes = its size.
+hipError_t work_malloc(int device, void **p, size_t need, size_t *bytes) {
+    if ((*p = spare_take(device, need, bytes)) != nullptr) return hipSuccess;
+    *bytes = need;
+    return hipMalloc(p, need);
 }
 
 bool fail(const char **errorMessage, const std::string &msg) {
@@ -447,28 +485,34 @@ void free_scene_buffers(Ctx &c) {
 
 void harvest_audit(Ctx &c);
 
-void destroy_ctx(Ctx &c) {
+// keep: the big work buffers go to State::spare (a re-initialization) instead of hipFree.
+void destroy_ctx(Ctx &c, bool keep) {
     (void)hipSetDevice(c.device);
-    if (c.stream) (void)hipStreamSynchronize(c.stream);
+    if (c.stream) (void)hipStreamSynchronize(c.stream);  // (so no queued launch reads a kept buffer)
+    auto drop = [&](void *p, size_t bytes) {
+        if (!p) return;
+        if (keep && bytes) S().spare.push_back({c.device, p, bytes});
+        else (void)hipFree(p);
+    };
     harvest_audit(c);  // closed runs' records; an open run's (its image discarded) are dropped
     (void)hipFree(c.auditDev);
     (void)hipFree(c.accum);
     (void)hipFree(c.out);
-    (void)hipFree(c.scratch);
-    (void)hipFree(c.scratchAlt);
+    drop(c.scratch, c.scratchBytes);
+    drop(c.scratchAlt, c.scratchAltBytes);
     c.scratchAlt = nullptr;
     c.scratchAltBytes = 0;
     c.hasDeferred = false;
     (void)hipFree(c.queue);
     (void)hipFree(c.chainCtl);
-    (void)hipFree(c.chainScratch);
+    drop(c.chainScratch, c.chainScratchBytes);
     if (c.chainBox) (void)hipHostFree(c.chainBox);
     if (c.chainStartEv) (void)hipEventDestroy(c.chainStartEv);
     if (c.chainEndEv) (void)hipEventDestroy(c.chainEndEv);
     (void)hipFree(c.stats);
     (void)hipFree(c.wfPool);
     (void)hipFree(c.wfCtr);
-    (void)hipFree(c.spill);
+    drop(c.spill, c.spillBytes);
     c.spill = nullptr;
     c.spillBytes = 0;
     (void)hipHostFree(c.wfHost);
@@ -486,9 +530,11 @@ void destroy_ctx(Ctx &c) {
     c = Ctx();
 }
 
-void destroy_all() {
+// keep: a re-initialization (init_inner) keeps the contexts' big work buffers for the new ones.
+void destroy_all(bool keep = false) {
     State &s = S();
-    for (auto &c : s.ctxs) destroy_ctx(c);
+    if (!keep) spare_free_all();
+    for (auto &c : s.ctxs) destroy_ctx(c, keep);
     s.ctxs.clear();
     for (auto &t : s.rngTables) {
         (void)hipSetDevice(t.first);
@@ -753,7 +799,8 @@ bool ensure_hybrid(Ctx &c, int top, const char **err) {
 
 bool init_inner(int width, int height, const char **err) {
     State &s = S();
-    destroy_all();
+    spare_free_all();   // the previous initialization's, none of which its contexts took again
+    destroy_all(true);  // this one's, for the new contexts
     if (width <= 0 || height <= 0) return fail(err, "invalid image size");
     s.width = width;
     s.height = height;
@@ -837,8 +884,9 @@ bool ensure_spill(Ctx &c, hippt::MeshParams &p, long long blocks, bool spills, i
         (void)hipFree(c.spill);
         c.spill = nullptr;
         c.spillBytes = 0;
-        HIP_TRY(hipMalloc(&c.spill, bytes));
-        c.spillBytes = bytes;
+        void *p = nullptr;
+        HIP_TRY(work_malloc(c.device, &p, bytes, &c.spillBytes));
+        c.spill = static_cast<int *>(p);
     }
     p.spill = c.spill;
     return true;
@@ -1081,8 +1129,9 @@ bool batch_scratch(Ctx &c, size_t need, float **out, const char **err) {
         (void)hipFree(buf);
         buf = nullptr;
         bytes = 0;
-        HIP_TRY(hipMalloc(&buf, need));
-        bytes = need;
+        void *p = nullptr;
+        HIP_TRY(work_malloc(c.device, &p, need, &bytes));
+        buf = static_cast<float *>(p);
     }
     *out = buf;
     return true;
@@ -1171,13 +1220,16 @@ bool ensure_ring(Ctx &c, const RingPlan &r, bool *ok, const char **err) {
     (void)hipFree(c.chainScratch);
     c.chainScratch = nullptr;
     c.chainScratchBytes = 0;
-    if (hipMalloc(&c.chainScratch, r.bytes) != hipSuccess) {
+    void *p = nullptr;
+    size_t got = 0;
+    if (work_malloc(c.device, &p, r.bytes, &got) != hipSuccess) {
         (void)hipGetLastError();
         c.chainScratch = nullptr;
         *ok = false;
         return true;
     }
-    c.chainScratchBytes = r.bytes;
+    c.chainScratch = static_cast<float *>(p);
+    c.chainScratchBytes = got;
     return true;
 }
 

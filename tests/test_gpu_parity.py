@@ -140,6 +140,26 @@ def test_mesh_matches_oracle(pt, name, w, h, spp, depth):
     assert st["segments"] == segs and st["pixelSamples"] == samples
 
 
+def test_reinitialize_reuses_work_buffers(pt):
+    """A re-initialization keeps the destroyed contexts' big work buffers (sample scratch, chain ring,
+    spill area) for the new contexts of the device (a fresh 13 GB ring took up to 5.9 s to allocate,
+    DESIGN_LOG.md §A.R6 r6af): sizes that grow and shrink, blocking and chained batches, blob70k's
+    spilling traversal and Cornell — every image the oracle's, whichever kept buffer it landed in."""
+    lib = hippt.load_library()
+    seq = [("blob70k", 64, 48, 3), ("blob70k", 20, 11, 2), ("cornell34", 96, 64, 2), ("blob70k", 80, 40, 3),
+           ("cornell34", 33, 17, 4), ("blob70k", 64, 48, 3)]
+    for name, w, h, frames in seq:
+        sc = scenes.get_scene(name)
+        pt.uploadMesh(sc)
+        assert pt.initialize(w, h), pt.lastError()
+        assert pt.renderFrames(1, 8), pt.lastError()  # blocking
+        for f in range(1, frames):  # then asynchronous one-frame batches (the chained path)
+            assert lib.hipptRenderFramesAsync(f, 1, 8, None), pt.lastError()
+        px, acc = pt.readback()
+        ora_px, ora_acc, _, _ = po.MeshScene(sc, w, h).frames(0, frames, 8)
+        _assert_same(px, acc, ora_px, ora_acc)
+
+
 @pytest.mark.parametrize("name,w,h,spp,depth,slots,width,cap", [
     ("cornell34", 96, 64, 8, 8, 1 << 21, 0, 0),
     ("cornell34", 33, 17, 3, 4, 64, 2, 0),

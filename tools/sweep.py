@@ -44,6 +44,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--blob", default=None, help="NU,NV: blob70k's walls + a blob of NU x NV quads")
     ap.add_argument("--count", action="store_true", help="report node visits / primitive tests per segment")
+    ap.add_argument("--prewarm-ms", type=float, default=200.0,
+                    help="untimed whole steps first (the GPU's clocks ramp over ~20 ms, DESIGN.md §6)")
     ap.add_argument("grid", nargs="*")
     a = ap.parse_args()
     axes = []
@@ -58,6 +60,12 @@ def main():
         sc = scenes.blob_scene(nu, nv)
         a.scene = f"blob{nu}x{nv}"
     pt.uploadMesh(sc)
+    if a.prewarm_ms > 0:
+        if not pt.initialize(a.width, a.height):
+            raise SystemExit(pt.lastError())
+        t0 = time.perf_counter()
+        while (time.perf_counter() - t0) * 1e3 < a.prewarm_ms:
+            pt.renderFrames(a.spp, a.depth, copy=False)
     for combo in itertools.product(*axes) if axes else [()]:
         for k, v in combo:
             pt.setOption(KEYS[k], v)
