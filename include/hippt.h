@@ -181,7 +181,9 @@ int hipptGetCounters(unsigned long long *out, int n);
 enum {
     HIPPT_OPT_COUNT_TRAVERSAL = 1,  /* 1: count node visits / triangle tests (slower) */
     HIPPT_OPT_WAVE_THRESHOLD = 2,   /* lanes still traversing below which a wave goes to shade; -1 (default):
-                                       16 for LDS-resident scenes, 32 otherwise */
+                                       24 for LDS-resident scenes and spheres / Metal / Dielectric, trees in
+                                       global memory 40 for megakernel batches of more than 2^26 samples,
+                                       else 32 */
     HIPPT_OPT_SCRATCH_MB = 3,       /* cap of the per-batch sample scratch per device (32768: one batch for 4K x 256 spp) */
     HIPPT_OPT_CHUNK = 4,            /* work items a wave takes from the global queue at once (64..2^20, a
                                        multiple of 64); 0 (default): automatic, 512 for chained or
