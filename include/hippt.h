@@ -198,9 +198,13 @@ enum {
     HIPPT_OPT_BVH_MAX_DEPTH = 12,   /* interior-level bound (LDS stack per lane), 1..32; next upload */
     HIPPT_OPT_DEVICE_ROWS = 13,     /* hipptSetDevices split: 1 (default) interleaved rows, 0 bands; next Init */
     HIPPT_OPT_LEAF_EXIT = 14        /* node loop yields to the leaf loop once <= this many lanes lack a
-                                       leaf; -1 (default): automatic (4 for LDS scenes, else levels-6 in 0..16) */
+                                       leaf; -1 (default): automatic (LDS scenes 12, 4 for the general kernel
+                                       and the wavefront; trees in global memory 12 for the general kernel,
+                                       22 for Lambertian megakernel batches of more than 2^26 samples, else 17) */
     , HIPPT_OPT_NODE_EXIT = 15      /* leaf loop yields to the node loop once <= this many lanes hold a leaf
-                                       (0 = never); -1 (default): 48 */
+                                       (0 = never); -1 (default): LDS scenes 8; trees in global memory 16 for
+                                       the general kernel, 56 for Lambertian megakernel batches of more than
+                                       2^26 samples, else 48 */
     , HIPPT_OPT_BVH_SAH = 16        /* BVH split search: 1 (default) all axes, exact sweep SAH (32 bins on
                                        nodes over 65536 primitives); 0: 16 bins on the longest axis; next upload */
     , HIPPT_OPT_BVH_WIDTH = 17      /* traversal over the 4-wide (4) or 2-wide (2) BVH (megakernel and wavefront);

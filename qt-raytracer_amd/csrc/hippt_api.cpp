@@ -1660,10 +1660,13 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         // 40 for the megakernel's batches of more than 2^26 samples (the wavefront
                         // keeps 32); Cornell 28/32 within 0.2% of 24.
                         const bool fullMega = s.pathMode == 0 && s.scene.full;
+                        // the Lambertian megakernel's big batches over a tree in global memory (this
+                        // wave threshold and the loop exits below)
+                        const bool bigGlobal = !ldsScene && !fullMega && s.pathMode == 0 && total > (1u << 26);
                         p.waveThreshold = s.waveThreshold >= 0    ? s.waveThreshold
                                           : ldsScene || fullMega ? 24
-                                          : s.pathMode == 0 && total > (1u << 26) ? 40
-                                                                                  : 32;
+                                          : bigGlobal            ? 40
+                                                                 : 32;
                         // claim size: 512 items for the Lambertian kernels' chained and whole-image
                         // batches (Cornell 1080p/64 spp 7.255 -> 7.199 ms, blob70k 18.94 -> 18.91,
                         // r5s; chained 1/8 shares Cornell 1.062 -> 1.041, blob70k 2.546 -> 2.547,
@@ -1683,13 +1686,20 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         // kernel and the wavefront keep leaf exit 4 (cornell_mixed +1.4%, Cornell
                         // wavefront +6% over 12; r6b)
                         // The general megakernel over a tree in global memory: 12 and 16 (random_scene,
-                        // r6c).
+                        // r6c).  With the wave threshold 40 of big batches, 22 and 56 (blob70k whole
+                        // image, alternating passes: 22,057 -> 22,372 M/s, +1.4%; 20-26 x 48-64 within
+                        // 0.3% of it, 28 lower, r6ao/r6ap).
                         const bool lambertMega = s.pathMode == 0 && !s.scene.full;
                         p.leafExit = unsigned(s.leafExit >= 0 ? s.leafExit
                                               : ldsScene          ? (lambertMega ? 12 : 4)
                                               : fullMega          ? 12
+                                              : bigGlobal         ? 22
                                                                   : 17);
-                        p.nodeExit = unsigned(s.nodeExit >= 0 ? s.nodeExit : ldsScene ? 8 : fullMega ? 16 : 48);
+                        p.nodeExit = unsigned(s.nodeExit >= 0 ? s.nodeExit
+                                              : ldsScene  ? 8
+                                              : fullMega  ? 16
+                                              : bigGlobal ? 56
+                                                          : 48);
                         p.wide = fmt;
                         p.stackCap = stackCap;
                         p.topBytes = topBytes;
