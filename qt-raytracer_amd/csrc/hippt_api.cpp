@@ -264,7 +264,7 @@ struct State {
     char error[256] = {0};
     // options
     bool countTraversal = false;
-    int waveThreshold = -1;  // -1: automatic (24 for LDS scenes and the general kernel; trees in global memory 40 for megakernel batches over 2^26 samples, else 32)
+    int waveThreshold = -1;  // -1: automatic (24 for LDS scenes and the general kernel; trees in global memory 40 for Lambertian batches over 2^26 samples, else 32)
     // one batch (and one end-of-batch tail) per call up to 4K/256 spp: 2.12G samples x 12 B
     long long scratchMB = 32768;
     unsigned chunk = 0;  // work items per claim (0: automatic, see enqueue_locked)
@@ -1657,12 +1657,12 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         // Re-swept on round 6's kernels (r6aj/r6ak, alternating passes): a whole
                         // blob70k image 40 over 32 +0.5-0.7% (21,882 -> 22,031 M/s; 36 +0.5%, 44 and 48
                         // slower), configs[3]'s 4K image +0.6%, but its 1/8 shares 2.433 -> 2.471 ms:
-                        // 40 for the megakernel's batches of more than 2^26 samples (the wavefront
-                        // keeps 32); Cornell 28/32 within 0.2% of 24.
+                        // 40 for batches of more than 2^26 samples; Cornell 28/32 within 0.2% of 24.
                         const bool fullMega = s.pathMode == 0 && s.scene.full;
-                        // the Lambertian megakernel's big batches over a tree in global memory (this
-                        // wave threshold and the loop exits below)
-                        const bool bigGlobal = !ldsScene && !fullMega && s.pathMode == 0 && total > (1u << 26);
+                        // big Lambertian batches over a tree in global memory, megakernel or wavefront
+                        // (this wave threshold and the loop exits below; the wavefront's configs[4]
+                        // 14,243 -> 14,436 M/s with 40 / 22 / 56, r6aq)
+                        const bool bigGlobal = !ldsScene && !s.scene.full && total > (1u << 26);
                         p.waveThreshold = s.waveThreshold >= 0    ? s.waveThreshold
                                           : ldsScene || fullMega ? 24
                                           : bigGlobal            ? 40
