@@ -181,9 +181,9 @@ int hipptGetCounters(unsigned long long *out, int n);
 enum {
     HIPPT_OPT_COUNT_TRAVERSAL = 1,  /* 1: count node visits / triangle tests (slower) */
     HIPPT_OPT_WAVE_THRESHOLD = 2,   /* lanes still traversing below which a wave goes to shade; -1 (default):
-                                       24 for LDS-resident scenes and spheres / Metal / Dielectric, trees in
-                                       global memory 40 for Lambertian batches of more than 2^26 samples
-                                       (megakernel and wavefront), else 32 */
+                                       24 for LDS-resident scenes and spheres / Metal / Dielectric over trees
+                                       in global memory, 40 for Lambertian scenes over trees in global memory
+                                       (32 before round 6) */
     HIPPT_OPT_SCRATCH_MB = 3,       /* cap of the per-batch sample scratch per device (32768: one batch for 4K x 256 spp) */
     HIPPT_OPT_CHUNK = 4,            /* work items a wave takes from the global queue at once (64..2^20, a
                                        multiple of 64); 0 (default): automatic, 512 for chained or
@@ -200,11 +200,10 @@ enum {
     HIPPT_OPT_LEAF_EXIT = 14        /* node loop yields to the leaf loop once <= this many lanes lack a
                                        leaf; -1 (default): automatic (LDS scenes 12, 4 for the general kernel
                                        and the wavefront; trees in global memory 12 for the general kernel,
-                                       22 for Lambertian batches of more than 2^26 samples, else 17) */
+                                       22 for Lambertian scenes (17 before round 6)) */
     , HIPPT_OPT_NODE_EXIT = 15      /* leaf loop yields to the node loop once <= this many lanes hold a leaf
                                        (0 = never); -1 (default): LDS scenes 8; trees in global memory 16 for
-                                       the general kernel, 56 for Lambertian batches of more than 2^26
-                                       samples, else 48 */
+                                       the general kernel, 56 for Lambertian scenes (48 before round 6) */
     , HIPPT_OPT_BVH_SAH = 16        /* BVH split search: 1 (default) all axes, exact sweep SAH (32 bins on
                                        nodes over 65536 primitives); 0: 16 bins on the longest axis; next upload */
     , HIPPT_OPT_BVH_WIDTH = 17      /* traversal over the 4-wide (4) or 2-wide (2) BVH (megakernel and wavefront);

@@ -264,7 +264,7 @@ struct State {
     char error[256] = {0};
     // options
     bool countTraversal = false;
-    int waveThreshold = -1;  // -1: automatic (24 for LDS scenes and the general kernel; trees in global memory 40 for Lambertian batches over 2^26 samples, else 32)
+    int waveThreshold = -1;  // -1: automatic (24 for LDS scenes and the general kernel, 40 for Lambertian scenes over trees in global memory)
     // one batch (and one end-of-batch tail) per call up to 4K/256 spp: 2.12G samples x 12 B
     long long scratchMB = 32768;
     unsigned chunk = 0;  // work items per claim (0: automatic, see enqueue_locked)
@@ -1657,15 +1657,17 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         // Re-swept on round 6's kernels (r6aj/r6ak, alternating passes): a whole
                         // blob70k image 40 over 32 +0.5-0.7% (21,882 -> 22,031 M/s; 36 +0.5%, 44 and 48
                         // slower), configs[3]'s 4K image +0.6%, but its 1/8 shares 2.433 -> 2.471 ms:
-                        // 40 for batches of more than 2^26 samples; Cornell 28/32 within 0.2% of 24.
+                        // 40 with the loop exits 22 / 56 below (alone, 40 slowed the shares: r6ak);
+                        // Cornell 28/32 within 0.2% of 24.
                         const bool fullMega = s.pathMode == 0 && s.scene.full;
-                        // big Lambertian batches over a tree in global memory, megakernel or wavefront
-                        // (this wave threshold and the loop exits below; the wavefront's configs[4]
-                        // 14,243 -> 14,436 M/s with 40 / 22 / 56, r6aq)
-                        const bool bigGlobal = !ldsScene && !s.scene.full && total > (1u << 26);
+                        // Lambertian batches over a tree in global memory, megakernel or wavefront (this
+                        // wave threshold and the loop exits below; the wavefront's configs[4] 14,243 ->
+                        // 14,436 M/s with 40 / 22 / 56, r6aq; blob70k's 1/4 and 1/8 row shares 4.705 ->
+                        // 4.612 and 2.433 -> 2.391 ms, r6at)
+                        const bool lambertGlobal = !ldsScene && !s.scene.full;
                         p.waveThreshold = s.waveThreshold >= 0    ? s.waveThreshold
                                           : ldsScene || fullMega ? 24
-                                          : bigGlobal            ? 40
+                                          : lambertGlobal        ? 40
                                                                  : 32;
                         // claim size: 512 items for the Lambertian kernels' chained and whole-image
                         // batches (Cornell 1080p/64 spp 7.255 -> 7.199 ms, blob70k 18.94 -> 18.91,
@@ -1686,20 +1688,20 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                         // kernel and the wavefront keep leaf exit 4 (cornell_mixed +1.4%, Cornell
                         // wavefront +6% over 12; r6b)
                         // The general megakernel over a tree in global memory: 12 and 16 (random_scene,
-                        // r6c).  With the wave threshold 40 of big batches, 22 and 56 (blob70k whole
-                        // image, alternating passes: 22,057 -> 22,372 M/s, +1.4%; 20-26 x 48-64 within
-                        // 0.3% of it, 28 lower, r6ao/r6ap).
+                        // r6c).  The Lambertian kernels over a tree in global memory, with the wave
+                        // threshold 40: 22 and 56 (blob70k whole image, alternating passes: 22,057 ->
+                        // 22,372 M/s, +1.4%; 20-26 x 48-64 within 0.3% of it, 28 lower, r6ao/r6ap).
                         const bool lambertMega = s.pathMode == 0 && !s.scene.full;
                         p.leafExit = unsigned(s.leafExit >= 0 ? s.leafExit
                                               : ldsScene          ? (lambertMega ? 12 : 4)
                                               : fullMega          ? 12
-                                              : bigGlobal         ? 22
+                                              : lambertGlobal     ? 22
                                                                   : 17);
                         p.nodeExit = unsigned(s.nodeExit >= 0 ? s.nodeExit
                                               : ldsScene  ? 8
                                               : fullMega  ? 16
-                                              : bigGlobal ? 56
-                                                          : 48);
+                                              : lambertGlobal ? 56
+                                                              : 48);
                         p.wide = fmt;
                         p.stackCap = stackCap;
                         p.topBytes = topBytes;
