@@ -259,9 +259,9 @@ enum {
                                        many (1..16), so that the run pays the launch's tail once per that many
                                        batches; the next launch combines them beside its own paths and the
                                        image's readers flush the rest.  0: one launch per batch; -1
-                                       (default): automatic (on for batches of at most 2^26 samples, for
-                                       trees in global memory and for the general kernel; 2..16 batches (8 over LDS-resident scenes) by
-                                       the batch's size).  Same results either way */
+                                       (default): automatic (on; 8 batches for batches of more than 2^26
+                                       samples, else 2..16 by the batch's size, at most 8 over LDS-resident
+                                       scenes).  Same results either way */
     , HIPPT_OPT_CHAIN_AUDIT = 31    /* 1: chained launches record, per batch of each run, the work items they
                                        traced (count and a hash of their indices), the frames and the launch
                                        they traced them with, and the pixels, frames and launch of the batch's

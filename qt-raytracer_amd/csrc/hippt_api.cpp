@@ -1137,18 +1137,15 @@ bool batch_scratch(Ctx &c, size_t need, float **out, const char **err) {
     return true;
 }
 
-// Chained batches (Ctx::chain).  Automatic: a launch traces up to ~4e8 samples' worth of batches (3 of
-// a whole 1080p/64 spp image, 8 of its 1/4 and 1/8 row shares); the ring holds twice that, so that a
-// launch traces one group of batches while it combines the previous one.
-// Automatic (HIPPT_OPT_CHAIN -1): chained batches for every batch of at most 2^26 samples (the row
-// shares of a 1080p/64 spp image split over 2 or more GPUs), for trees in global memory and for the
-// general kernel (spheres, Metal/Dielectric); a whole image of an LDS-resident Lambertian scene runs
-// one launch per batch.  Measured (r5s/r5x, 20 steps, cap by chain_cap): 1/8 shares Cornell 1.112 ->
-// 1.047 ms, blob70k 3.003 -> 2.518, cornell_mixed 1.831 -> 1.573; 1/2 shares blob70k 9.79 -> 9.49,
-// cornell_mixed 6.20 -> 5.92, Cornell 3.757 -> 3.765; whole images blob70k 18.94 -> 18.69,
-// cornell_mixed 12.06 -> 11.70, but Cornell 7.255 -> 7.321: a whole Cornell batch has little tail to
-// save, and a run pays its first launch's start and its last group's combine without overlap.
-bool chain_auto(unsigned total, bool ldsScene, bool full) { return total <= (1u << 26) || !ldsScene || full; }
+// Chained batches (Ctx::chain).  Automatic (HIPPT_OPT_CHAIN -1): every batch (whose items fit the ring's
+// slot bits) is chained; a launch traces up to cap batches (chain_cap) and the ring holds twice that, so
+// that a launch traces one group of batches while it combines the previous one.  Measured (r5s/r5x, 20
+// steps, cap by chain_cap): 1/8 shares Cornell 1.112 -> 1.047 ms, blob70k 3.003 -> 2.518, cornell_mixed
+// 1.831 -> 1.573; 1/2 shares blob70k 9.79 -> 9.49, cornell_mixed 6.20 -> 5.92, Cornell 3.757 -> 3.765;
+// whole images blob70k 18.94 -> 18.69, cornell_mixed 12.06 -> 11.70, but Cornell 7.255 -> 7.321, so
+// round 5 ran a whole image of an LDS-resident Lambertian scene one launch per batch.  Round 6 (r6aw/r6ax,
+// alternating passes, with the held groups and the clock warm-up): a whole Cornell image chained at cap 8
+// 55,875 -> 56,111 M/s, so it is chained too.
 // chain_batch's held groups (an A/B build knob)
 #ifndef HIPPT_CHAIN_GROUPS
 #define HIPPT_CHAIN_GROUPS 1
@@ -1166,9 +1163,12 @@ constexpr bool kChainHoldRunning = HIPPT_CHAIN_HOLD_RUNNING != 0;
 // (blob70k 1/8 share 2.538/2.539 -> 2.497/2.493 ms, 1/4 share 4.799/4.778 -> 4.754/4.754), exposed
 // beside Cornell's (1/8 share 0.991/0.989 -> 1.025/1.015: the last launch's 16-batch combine adds
 // ~0.9 ms), r6n.
+// Batches of more than 2^26 samples (whole 1080p/64 spp images) take cap 8 (r6aw/r6ax: blob70k 22,302 ->
+// 22,391 M/s against cap 3, cornell_mixed 35,314 -> 35,422, Cornell chained at 8 as above; cap 2 and 6
+// lower or equal); the ring (16 slots) stays within the scratch budget (ring_plan) or the cap shrinks.
 unsigned chain_cap(long long option, unsigned total, bool ldsScene) {
     if (option > 0) return unsigned(std::min<long long>(option, 16));
-    const double c = std::round(4e8 / double(std::max(1u, total)));
+    const double c = total > (1u << 26) ? 8.0 : std::round(4e8 / double(std::max(1u, total)));
     return unsigned(std::clamp(c, 2.0, ldsScene ? 8.0 : 16.0));
 }
 
@@ -1600,7 +1600,7 @@ bool enqueue_locked(int firstFrame, int count, int maxDepth, bool copy, const ch
                     const bool fuse = maxDepth > 0 && s.pathMode == 0 && s.fuseCombine != 0;
                     // chained batches (Ctx::chain): asynchronous camera-pool megakernel batches over
                     // 4-wide float nodes whose items fit the ring's slot bits
-                    bool chained = fuse && !copy && !cnt && (s.chainBatches > 0 || (s.chainBatches < 0 && chain_auto(total, ldsScene, s.scene.full))) &&
+                    bool chained = fuse && !copy && !cnt && s.chainBatches != 0 &&
                                    poolWords != 0 &&
                                    fmt == hippt::kWideFloat && c.meshBlocksPerCuChain > 0 &&
                                    total <= (1u << hippt::kChainMaxShift);

@@ -800,16 +800,16 @@ def test_chained_batches_camera_change_and_row_shares(pt):
 
 def test_automatic_chain_and_claim_size(pt):
     """HIPPT_OPT_CHAIN -1 and HIPPT_OPT_CHUNK 0 (the defaults) as applied (HIPPT_INFO_CHAIN_CAP,
-    HIPPT_INFO_CHUNK): a whole 1080p/64 spp Cornell batch runs unchained with 512-item claims; its 1/8
-    row share chains 8 batches, also with 512-item claims; blob70k's whole image (a tree in global
-    memory) and cornell_mixed's (the general kernel, 256-item claims) chain 3, blob70k's 1/8 share 16
-    (the automatic cap's ceiling for trees in global memory)."""
+    HIPPT_INFO_CHUNK): a whole 1080p/64 spp image chains 8 batches (round 6; Cornell ran unchained and
+    blob70k / cornell_mixed chained 3 before), Cornell and blob70k with 512-item claims, cornell_mixed
+    (the general kernel) with 256; Cornell's 1/8 row share chains 8, blob70k's 16 (the automatic cap's
+    ceiling for trees in global memory)."""
     lib = hippt.load_library()
     pt.setOption(hippt.OPT_CHAIN, -1)
     pt.setOption(hippt.OPT_CHUNK, 0)
-    for name, stride, cap, chunk in (("cornell34", 1, 0, 512), ("cornell34", 8, 8, 512), ("blob70k", 1, 3, 512),
+    for name, stride, cap, chunk in (("cornell34", 1, 8, 512), ("cornell34", 8, 8, 512), ("blob70k", 1, 8, 512),
                                      ("blob70k", 8, 16, 512),
-                                     ("cornell_mixed", 1, 3, 256)):
+                                     ("cornell_mixed", 1, 8, 256)):
         pt.uploadMesh(scenes.get_scene(name))
         pt.setRowInterleave(0, stride)
         assert pt.initialize(1920, 1080)
