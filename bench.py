@@ -88,8 +88,10 @@ def log(*a):
 def parse():
     p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=2)
+    # the driver's round-end run is 20 timed steps; with chained batches (up to 8 whole images per
+    # launch) fewer steps weigh the run's first and last launch more (10 steps: 55.4 G, r6ba)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--prewarm-ms", type=float, default=200.0,
                    help="untimed GPU clock warm-up before the warmup steps: whole steps for this many ms")
     p.add_argument("--scene", default="cornell34",
