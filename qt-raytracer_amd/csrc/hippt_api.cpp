@@ -338,11 +338,17 @@ void spare_free_all() {
     S().spare.clear();
 }
 
-// hipMalloc of a big work buffer, or a kept one of the same device (spare_take); *bytes = its size.
+// hipMalloc of a big work buffer, or a kept one of the same device (spare_take); *bytes = its size,
+// set only on success (a failed allocation leaves the caller's buffer empty, size 0).
 hipError_t work_malloc(int device, void **p, size_t need, size_t *bytes) {
     if ((*p = spare_take(device, need, bytes)) != nullptr) return hipSuccess;
+    const hipError_t e = hipMalloc(p, need);
+    if (e != hipSuccess) {
+        *p = nullptr;
+        return e;
+    }
     *bytes = need;
-    return hipMalloc(p, need);
+    return hipSuccess;
 }
 
 bool fail(const char **errorMessage, const std::string &msg) {
